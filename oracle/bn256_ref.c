@@ -1,0 +1,1256 @@
+/*
+ * bn256_ref.c — CPU restatement of the Handel BN256 BLS verification path.
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/ (as the checker) and by
+ * bench.py's cpu_baseline leg (timed as "port" of the reference algorithm).
+ * The product library (handel_amd/csrc) never links or calls this file.
+ *
+ * It restates, in plain C with 4x64-bit Montgomery arithmetic, exactly what
+ * oracle/bn256_oracle.py restates (see that file's header for the upstream
+ * module pins and the parity status, "parity unpinned by known-answer
+ * vectors"):
+ *   - x/crypto/bn256 optimal-ate pairing (optate.go lineFunctionDouble,
+ *     lineFunctionAdd, mulLine, miller, finalExponentiation),
+ *   - bn256/go/bn256.go:82-94 VerifySignature (two full pairings, GT compare),
+ *   - bn256/go/bn256.go:210-218 hashedMessage with the crypto/rand.Int rule,
+ *   - bn256/go/bn256.go:97-105, 192-200 G2 / G1 Combine,
+ *   - processing.go:342-368 verifySignature over a level range + bitset.
+ * Build: oracle/Makefile -> oracle/_build/libbn256_ref.so
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+typedef unsigned __int128 u128;
+typedef struct { uint64_t v[4]; } fp;
+typedef struct { fp x, y; } fp2;           /* x*i + y */
+typedef struct { fp2 c[6]; } fp12;         /* flat over omega^k, omega^6 = xi */
+typedef struct { fp2 x, y, z, t; } g2p;    /* twist point, Jacobian, t = z^2 */
+typedef struct { fp x, y, z; } g1p;        /* Jacobian */
+
+/* p (little-endian 64-bit limbs) */
+static const fp P_ = {{0x185cac6c5e089667ULL, 0xee5b88d120b5b59eULL,
+                       0xaa6fecb86184dc21ULL, 0x8fb501e34aa387f9ULL}};
+static uint64_t PINV; /* -p^-1 mod 2^64 */
+static fp R2;         /* 2^512 mod p */
+static fp ONE_M;      /* 2^256 mod p (Montgomery one) */
+static int g_inited = 0;
+
+/* ------------------------------------------------------------------ Fp */
+static inline int fp_geq_p(const uint64_t* t) {
+  for (int i = 3; i >= 0; i--) {
+    if (t[i] > P_.v[i]) return 1;
+    if (t[i] < P_.v[i]) return 0;
+  }
+  return 1;
+}
+static inline void fp_sub_p(uint64_t* t) {
+  u128 b = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 d = (u128)t[i] - P_.v[i] - b;
+    t[i] = (uint64_t)d;
+    b = (d >> 64) & 1;
+  }
+}
+static inline void fp_add(fp* r, const fp* a, const fp* b) {
+  uint64_t t[4];
+  u128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    c += (u128)a->v[i] + b->v[i];
+    t[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  if (c || fp_geq_p(t)) fp_sub_p(t);
+  memcpy(r->v, t, 32);
+}
+static inline void fp_sub(fp* r, const fp* a, const fp* b) {
+  uint64_t t[4];
+  u128 bw = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 d = (u128)a->v[i] - b->v[i] - bw;
+    t[i] = (uint64_t)d;
+    bw = (d >> 64) & 1;
+  }
+  if (bw) {
+    u128 c = 0;
+    for (int i = 0; i < 4; i++) {
+      c += (u128)t[i] + P_.v[i];
+      t[i] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  memcpy(r->v, t, 32);
+}
+static inline int fp_is_zero(const fp* a) { return (a->v[0] | a->v[1] | a->v[2] | a->v[3]) == 0; }
+static inline int fp_eq(const fp* a, const fp* b) { return memcmp(a, b, 32) == 0; }
+static inline void fp_neg(fp* r, const fp* a) {
+  fp z = {{0, 0, 0, 0}};
+  fp_sub(r, &z, a);
+}
+/* CIOS Montgomery multiplication, R = 2^256 */
+static inline void fp_mul(fp* r, const fp* a, const fp* b) {
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 4; j++) {
+      c = (u128)a->v[j] * b->v[i] + t[j] + (uint64_t)(c >> 64);
+      t[j] = (uint64_t)c;
+    }
+    c = (u128)t[4] + (uint64_t)(c >> 64);
+    t[4] = (uint64_t)c;
+    t[5] = (uint64_t)(c >> 64);
+    uint64_t m = t[0] * PINV;
+    c = (u128)m * P_.v[0] + t[0];
+    for (int j = 1; j < 4; j++) {
+      c = (u128)m * P_.v[j] + t[j] + (uint64_t)(c >> 64);
+      t[j - 1] = (uint64_t)c;
+    }
+    c = (u128)t[4] + (uint64_t)(c >> 64);
+    t[3] = (uint64_t)c;
+    t[4] = t[5] + (uint64_t)(c >> 64);
+  }
+  if (t[4] || fp_geq_p(t)) fp_sub_p(t);
+  memcpy(r->v, t, 32);
+}
+static inline void fp_sqr(fp* r, const fp* a) { fp_mul(r, a, a); }
+static void fp_from_u64(fp* r, uint64_t x) {
+  fp t = {{x, 0, 0, 0}};
+  fp_mul(r, &t, &R2);
+}
+static void fp_pow(fp* r, const fp* a, const uint64_t e[4]) {
+  fp acc = ONE_M, b = *a;
+  for (int i = 3; i >= 0; i--)
+    for (int bit = 63; bit >= 0; bit--) {
+      fp_sqr(&acc, &acc);
+      if ((e[i] >> bit) & 1) fp_mul(&acc, &acc, &b);
+    }
+  *r = acc;
+}
+static void fp_inv(fp* r, const fp* a) {
+  uint64_t e[4];
+  memcpy(e, P_.v, 32);
+  e[0] -= 2;
+  fp_pow(r, a, e);
+}
+/* bytes (32 BE) -> canonical integer limbs; returns 1 if value >= p */
+static int int_from_be(uint64_t t[4], const uint8_t* b) {
+  for (int i = 0; i < 4; i++) {
+    uint64_t w = 0;
+    for (int k = 0; k < 8; k++) w = (w << 8) | b[(3 - i) * 8 + k];
+    t[i] = w;
+  }
+  return fp_geq_p(t);
+}
+static void fp_to_mont(fp* r, const uint64_t t[4]) {
+  fp x;
+  memcpy(x.v, t, 32);
+  if (fp_geq_p(x.v)) fp_sub_p(x.v); /* value < 2^256 < 2p */
+  fp_mul(r, &x, &R2);
+}
+static void fp_from_mont(uint64_t t[4], const fp* a) {
+  fp one = {{1, 0, 0, 0}}, x;
+  fp_mul(&x, a, &one);
+  memcpy(t, x.v, 32);
+}
+static void fp_to_be(uint8_t* b, const fp* a) {
+  uint64_t t[4];
+  fp_from_mont(t, a);
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 8; k++) b[(3 - i) * 8 + k] = (uint8_t)(t[i] >> (56 - 8 * k));
+}
+
+/* ------------------------------------------------------------------ Fp2 */
+static inline void f2_add(fp2* r, const fp2* a, const fp2* b) { fp_add(&r->x, &a->x, &b->x); fp_add(&r->y, &a->y, &b->y); }
+static inline void f2_sub(fp2* r, const fp2* a, const fp2* b) { fp_sub(&r->x, &a->x, &b->x); fp_sub(&r->y, &a->y, &b->y); }
+static inline void f2_neg(fp2* r, const fp2* a) { fp_neg(&r->x, &a->x); fp_neg(&r->y, &a->y); }
+static inline void f2_dbl(fp2* r, const fp2* a) { f2_add(r, a, a); }
+static inline void f2_mul(fp2* r, const fp2* a, const fp2* b) {
+  fp t0, t1, t2, s0, s1;
+  fp_mul(&t0, &a->y, &b->y);
+  fp_mul(&t1, &a->x, &b->x);
+  fp_add(&s0, &a->x, &a->y);
+  fp_add(&s1, &b->x, &b->y);
+  fp_mul(&t2, &s0, &s1);
+  fp_sub(&r->y, &t0, &t1);
+  fp_sub(&t2, &t2, &t0);
+  fp_sub(&r->x, &t2, &t1);
+}
+static inline void f2_sqr(fp2* r, const fp2* a) {
+  fp s, d, m;
+  fp_add(&s, &a->y, &a->x);
+  fp_sub(&d, &a->y, &a->x);
+  fp_mul(&m, &a->x, &a->y);
+  fp_mul(&r->y, &s, &d);
+  fp_add(&r->x, &m, &m);
+}
+static inline void f2_muls(fp2* r, const fp2* a, const fp* s) { fp_mul(&r->x, &a->x, s); fp_mul(&r->y, &a->y, s); }
+static inline void f2_mul_xi(fp2* r, const fp2* a) {
+  /* (x i + y)(i + 3) = (3x + y) i + (3y - x) */
+  fp x3, y3, nx, ny;
+  fp_add(&x3, &a->x, &a->x);
+  fp_add(&x3, &x3, &a->x);
+  fp_add(&y3, &a->y, &a->y);
+  fp_add(&y3, &y3, &a->y);
+  fp_add(&nx, &x3, &a->y);
+  fp_sub(&ny, &y3, &a->x);
+  r->x = nx;
+  r->y = ny;
+}
+static inline void f2_conj(fp2* r, const fp2* a) { fp_neg(&r->x, &a->x); r->y = a->y; }
+static void f2_inv(fp2* r, const fp2* a) {
+  fp t, u, n;
+  fp_sqr(&t, &a->x);
+  fp_sqr(&u, &a->y);
+  fp_add(&n, &t, &u);
+  fp_inv(&n, &n);
+  fp nx;
+  fp_neg(&nx, &a->x);
+  fp_mul(&r->x, &nx, &n);
+  fp_mul(&r->y, &a->y, &n);
+}
+static inline int f2_is_zero(const fp2* a) { return fp_is_zero(&a->x) && fp_is_zero(&a->y); }
+static inline int f2_eq(const fp2* a, const fp2* b) { return fp_eq(&a->x, &b->x) && fp_eq(&a->y, &b->y); }
+
+/* constants (Montgomery form), initialised in ref_init() */
+static fp2 F2_ONE, F2_ZERO, TWIST_B, XI_P13, XI_P12, GAMMA1[6];
+static fp XI_PSQ13, GAMMA2[6], CURVE_B;
+static fp2 G2X, G2Y;
+static fp G1X, G1Y;
+
+/* ------------------------------------------------------------------ Fp6/Fp12 (Karatsuba tower view) */
+typedef struct { fp2 c[3]; } fp6; /* c0 + c1 tau + c2 tau^2 */
+static inline void f6_add(fp6* r, const fp6* a, const fp6* b) { for (int i = 0; i < 3; i++) f2_add(&r->c[i], &a->c[i], &b->c[i]); }
+static inline void f6_sub(fp6* r, const fp6* a, const fp6* b) { for (int i = 0; i < 3; i++) f2_sub(&r->c[i], &a->c[i], &b->c[i]); }
+static void f6_mul(fp6* r, const fp6* a, const fp6* b) {
+  fp2 v0, v1, v2, t0, t1, t2, s;
+  f2_mul(&v0, &a->c[0], &b->c[0]);
+  f2_mul(&v1, &a->c[1], &b->c[1]);
+  f2_mul(&v2, &a->c[2], &b->c[2]);
+  /* c0 = v0 + xi((a1+a2)(b1+b2) - v1 - v2) */
+  f2_add(&t0, &a->c[1], &a->c[2]);
+  f2_add(&s, &b->c[1], &b->c[2]);
+  f2_mul(&t0, &t0, &s);
+  f2_sub(&t0, &t0, &v1);
+  f2_sub(&t0, &t0, &v2);
+  f2_mul_xi(&t0, &t0);
+  f2_add(&t0, &t0, &v0);
+  /* c1 = (a0+a1)(b0+b1) - v0 - v1 + xi v2 */
+  f2_add(&t1, &a->c[0], &a->c[1]);
+  f2_add(&s, &b->c[0], &b->c[1]);
+  f2_mul(&t1, &t1, &s);
+  f2_sub(&t1, &t1, &v0);
+  f2_sub(&t1, &t1, &v1);
+  f2_mul_xi(&s, &v2);
+  f2_add(&t1, &t1, &s);
+  /* c2 = (a0+a2)(b0+b2) - v0 - v2 + v1 */
+  f2_add(&t2, &a->c[0], &a->c[2]);
+  f2_add(&s, &b->c[0], &b->c[2]);
+  f2_mul(&t2, &t2, &s);
+  f2_sub(&t2, &t2, &v0);
+  f2_sub(&t2, &t2, &v2);
+  f2_add(&t2, &t2, &v1);
+  r->c[0] = t0;
+  r->c[1] = t1;
+  r->c[2] = t2;
+}
+static inline void f6_mul_tau(fp6* r, const fp6* a) {
+  fp2 t;
+  f2_mul_xi(&t, &a->c[2]);
+  r->c[2] = a->c[1];
+  r->c[1] = a->c[0];
+  r->c[0] = t;
+}
+static inline void split12(const fp12* a, fp6* A, fp6* B) {
+  A->c[0] = a->c[0]; A->c[1] = a->c[2]; A->c[2] = a->c[4];
+  B->c[0] = a->c[1]; B->c[1] = a->c[3]; B->c[2] = a->c[5];
+}
+static inline void join12(fp12* r, const fp6* A, const fp6* B) {
+  r->c[0] = A->c[0]; r->c[2] = A->c[1]; r->c[4] = A->c[2];
+  r->c[1] = B->c[0]; r->c[3] = B->c[1]; r->c[5] = B->c[2];
+}
+static void f12_mul(fp12* r, const fp12* a, const fp12* b) {
+  fp6 A, B, C, D, AC, BD, S, T;
+  split12(a, &A, &B);
+  split12(b, &C, &D);
+  f6_mul(&AC, &A, &C);
+  f6_mul(&BD, &B, &D);
+  f6_add(&S, &A, &B);
+  f6_add(&T, &C, &D);
+  f6_mul(&S, &S, &T);
+  f6_sub(&S, &S, &AC);
+  f6_sub(&S, &S, &BD);
+  f6_mul_tau(&BD, &BD);
+  f6_add(&AC, &AC, &BD);
+  join12(r, &AC, &S);
+}
+static void f12_sqr(fp12* r, const fp12* a) {
+  /* complex squaring: (A + Bw)^2 = (A+B)(A+tau B) - AB - tau AB + 2AB w */
+  fp6 A, B, AB, t0, t1;
+  split12(a, &A, &B);
+  f6_mul(&AB, &A, &B);
+  f6_add(&t0, &A, &B);
+  f6_mul_tau(&t1, &B);
+  f6_add(&t1, &t1, &A);
+  f6_mul(&t0, &t0, &t1);
+  f6_sub(&t0, &t0, &AB);
+  f6_mul_tau(&t1, &AB);
+  f6_sub(&t0, &t0, &t1);
+  f6_add(&AB, &AB, &AB);
+  join12(r, &t0, &AB);
+}
+static void f12_one(fp12* r) {
+  for (int k = 0; k < 6; k++) r->c[k] = F2_ZERO;
+  r->c[0] = F2_ONE;
+}
+static int f12_is_one(const fp12* a) {
+  if (!f2_eq(&a->c[0], &F2_ONE)) return 0;
+  for (int k = 1; k < 6; k++)
+    if (!f2_is_zero(&a->c[k])) return 0;
+  return 1;
+}
+static void f12_conj(fp12* r, const fp12* a) {
+  for (int k = 0; k < 6; k++) {
+    if (k & 1) f2_neg(&r->c[k], &a->c[k]);
+    else r->c[k] = a->c[k];
+  }
+}
+static void f12_frob(fp12* r, const fp12* a) {
+  for (int k = 0; k < 6; k++) {
+    fp2 t;
+    f2_conj(&t, &a->c[k]);
+    f2_mul(&r->c[k], &t, &GAMMA1[k]);
+  }
+}
+static void f12_frob2(fp12* r, const fp12* a) {
+  for (int k = 0; k < 6; k++) f2_muls(&r->c[k], &a->c[k], &GAMMA2[k]);
+}
+static void f6_inv(fp6* r, const fp6* a) {
+  fp2 t0, t1, t2, s, d;
+  f2_sqr(&t0, &a->c[0]);
+  f2_mul(&s, &a->c[1], &a->c[2]);
+  f2_mul_xi(&s, &s);
+  f2_sub(&t0, &t0, &s);
+  f2_sqr(&t1, &a->c[2]);
+  f2_mul_xi(&t1, &t1);
+  f2_mul(&s, &a->c[0], &a->c[1]);
+  f2_sub(&t1, &t1, &s);
+  f2_sqr(&t2, &a->c[1]);
+  f2_mul(&s, &a->c[0], &a->c[2]);
+  f2_sub(&t2, &t2, &s);
+  f2_mul(&d, &a->c[2], &t1);
+  f2_mul(&s, &a->c[1], &t2);
+  f2_add(&d, &d, &s);
+  f2_mul_xi(&d, &d);
+  f2_mul(&s, &a->c[0], &t0);
+  f2_add(&d, &d, &s);
+  f2_inv(&d, &d);
+  f2_mul(&r->c[0], &t0, &d);
+  f2_mul(&r->c[1], &t1, &d);
+  f2_mul(&r->c[2], &t2, &d);
+}
+static void f12_inv(fp12* r, const fp12* a) {
+  fp6 A, B, AA, BB, ni;
+  split12(a, &A, &B);
+  f6_mul(&AA, &A, &A);
+  f6_mul(&BB, &B, &B);
+  f6_mul_tau(&BB, &BB);
+  f6_sub(&AA, &AA, &BB);
+  f6_inv(&ni, &AA);
+  f6_mul(&A, &A, &ni);
+  f6_mul(&B, &B, &ni);
+  for (int i = 0; i < 3; i++) f2_neg(&B.c[i], &B.c[i]);
+  join12(r, &A, &B);
+}
+static void f12_pow_u(fp12* r, const fp12* a) {
+  /* gfP12.Exp(a, u): MSB-first square-and-multiply */
+  const uint64_t u = 6518589491078791937ULL;
+  fp12 acc;
+  f12_one(&acc);
+  for (int bit = 63; bit >= 0; bit--) {
+    f12_sqr(&acc, &acc);
+    if ((u >> bit) & 1) f12_mul(&acc, &acc, a);
+  }
+  *r = acc;
+}
+static void f12_mul_line(fp12* f, const fp2* a, const fp2* b, const fp2* c) {
+  fp12 l;
+  for (int k = 0; k < 6; k++) l.c[k] = F2_ZERO;
+  l.c[0] = *c;
+  l.c[1] = *b;
+  l.c[3] = *a;
+  f12_mul(f, f, &l);
+}
+
+/* ------------------------------------------------------------------ Miller loop (optate.go) */
+static void line_double(fp2* a, fp2* b, fp2* c, g2p* r, const fp* qx, const fp* qy) {
+  fp2 A, B, C, D, E, G, t, xo, yo, zo, to;
+  f2_sqr(&A, &r->x);
+  f2_sqr(&B, &r->y);
+  f2_sqr(&C, &B);
+  f2_add(&D, &r->x, &B);
+  f2_sqr(&D, &D);
+  f2_sub(&D, &D, &A);
+  f2_sub(&D, &D, &C);
+  f2_dbl(&D, &D);
+  f2_add(&E, &A, &A);
+  f2_add(&E, &E, &A);
+  f2_sqr(&G, &E);
+  f2_sub(&xo, &G, &D);
+  f2_sub(&xo, &xo, &D);
+  f2_add(&zo, &r->y, &r->z);
+  f2_sqr(&zo, &zo);
+  f2_sub(&zo, &zo, &B);
+  f2_sub(&zo, &zo, &r->t);
+  f2_sub(&yo, &D, &xo);
+  f2_mul(&yo, &yo, &E);
+  f2_dbl(&t, &C);
+  f2_dbl(&t, &t);
+  f2_dbl(&t, &t);
+  f2_sub(&yo, &yo, &t);
+  f2_sqr(&to, &zo);
+  f2_mul(&t, &E, &r->t);
+  f2_dbl(&t, &t);
+  f2_neg(&t, &t);
+  f2_muls(b, &t, qx);
+  f2_add(a, &r->x, &E);
+  f2_sqr(a, a);
+  f2_sub(a, a, &A);
+  f2_sub(a, a, &G);
+  f2_dbl(&t, &B);
+  f2_dbl(&t, &t);
+  f2_sub(a, a, &t);
+  f2_mul(c, &zo, &r->t);
+  f2_dbl(c, c);
+  f2_muls(c, c, qy);
+  r->x = xo; r->y = yo; r->z = zo; r->t = to;
+}
+static void line_add(fp2* a, fp2* b, fp2* c, g2p* r, const fp2* px, const fp2* py,
+                     const fp* qx, const fp* qy, const fp2* r2) {
+  fp2 B, D, H, I, E, J, L1, V, t, t2, xo, yo, zo, to;
+  f2_mul(&B, px, &r->t);
+  f2_add(&D, py, &r->z);
+  f2_sqr(&D, &D);
+  f2_sub(&D, &D, r2);
+  f2_sub(&D, &D, &r->t);
+  f2_mul(&D, &D, &r->t);
+  f2_sub(&H, &B, &r->x);
+  f2_sqr(&I, &H);
+  f2_dbl(&E, &I);
+  f2_dbl(&E, &E);
+  f2_mul(&J, &H, &E);
+  f2_sub(&L1, &D, &r->y);
+  f2_sub(&L1, &L1, &r->y);
+  f2_mul(&V, &r->x, &E);
+  f2_sqr(&xo, &L1);
+  f2_sub(&xo, &xo, &J);
+  f2_sub(&xo, &xo, &V);
+  f2_sub(&xo, &xo, &V);
+  f2_add(&zo, &r->z, &H);
+  f2_sqr(&zo, &zo);
+  f2_sub(&zo, &zo, &r->t);
+  f2_sub(&zo, &zo, &I);
+  f2_sub(&t, &V, &xo);
+  f2_mul(&t, &t, &L1);
+  f2_mul(&t2, &r->y, &J);
+  f2_dbl(&t2, &t2);
+  f2_sub(&yo, &t, &t2);
+  f2_sqr(&to, &zo);
+  f2_add(&t, py, &zo);
+  f2_sqr(&t, &t);
+  f2_sub(&t, &t, r2);
+  f2_sub(&t, &t, &to);
+  f2_mul(&t2, &L1, px);
+  f2_dbl(&t2, &t2);
+  f2_sub(a, &t2, &t);
+  f2_muls(c, &zo, qy);
+  f2_dbl(c, c);
+  f2_neg(&t, &L1);
+  f2_muls(b, &t, qx);
+  f2_dbl(b, b);
+  r->x = xo; r->y = yo; r->z = zo; r->t = to;
+}
+
+static const int8_t NAF[66] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0, -1, 0, 1, 0, 1, 0,
+                               0, 0, 0, 1, 0, 1, 0, 0, 0, -1, 0, 1, 0, 0, 0, 1, 0, -1, 0, 0, 0, -1,
+                               0, 1, 0, 0, 0, 0, 0, 1, 0, 0, -1, 0, -1, 0, 0, 0, 0, 1, 0, 0, 0, 1};
+
+/* qx2/qy2: affine twist point; px/py: affine G1 point */
+static void miller(fp12* f, const fp2* qx2, const fp2* qy2, const fp* px, const fp* py) {
+  g2p r;
+  fp2 a, b, c, r2, mqy;
+  r.x = *qx2; r.y = *qy2; r.z = F2_ONE; r.t = F2_ONE;
+  f2_sqr(&r2, qy2);
+  f2_neg(&mqy, qy2);
+  f12_one(f);
+  for (int i = 65; i > 0; i--) {
+    line_double(&a, &b, &c, &r, px, py);
+    if (i != 65) f12_sqr(f, f);
+    f12_mul_line(f, &a, &b, &c);
+    int d = NAF[i - 1];
+    if (d == 0) continue;
+    line_add(&a, &b, &c, &r, qx2, d > 0 ? qy2 : &mqy, px, py, &r2);
+    f12_mul_line(f, &a, &b, &c);
+  }
+  fp2 q1x, q1y, q2x;
+  f2_conj(&q1x, qx2);
+  f2_mul(&q1x, &q1x, &XI_P13);
+  f2_conj(&q1y, qy2);
+  f2_mul(&q1y, &q1y, &XI_P12);
+  f2_sqr(&r2, &q1y);
+  line_add(&a, &b, &c, &r, &q1x, &q1y, px, py, &r2);
+  f12_mul_line(f, &a, &b, &c);
+  f2_muls(&q2x, qx2, &XI_PSQ13);
+  f2_sqr(&r2, qy2);
+  line_add(&a, &b, &c, &r, &q2x, qy2, px, py, &r2);
+  f12_mul_line(f, &a, &b, &c);
+}
+
+static void final_exp(fp12* out, const fp12* in) {
+  fp12 t1, inv, t2, fp_, fp2_, fp3, fu, fu2, fu3, y0, y1, y2, y3, y4, y5, y6, fu2p, fu3p, t0;
+  f12_conj(&t1, in);
+  f12_inv(&inv, in);
+  f12_mul(&t1, &t1, &inv);
+  f12_frob2(&t2, &t1);
+  f12_mul(&t1, &t1, &t2);
+  f12_frob(&fp_, &t1);
+  f12_frob2(&fp2_, &t1);
+  f12_frob(&fp3, &fp2_);
+  f12_pow_u(&fu, &t1);
+  f12_pow_u(&fu2, &fu);
+  f12_pow_u(&fu3, &fu2);
+  f12_frob(&y3, &fu);
+  f12_frob(&fu2p, &fu2);
+  f12_frob(&fu3p, &fu3);
+  f12_frob2(&y2, &fu2);
+  f12_mul(&y0, &fp_, &fp2_);
+  f12_mul(&y0, &y0, &fp3);
+  f12_conj(&y1, &t1);
+  f12_conj(&y5, &fu2);
+  f12_conj(&y3, &y3);
+  f12_mul(&y4, &fu, &fu2p);
+  f12_conj(&y4, &y4);
+  f12_mul(&y6, &fu3, &fu3p);
+  f12_conj(&y6, &y6);
+  f12_sqr(&t0, &y6);
+  f12_mul(&t0, &t0, &y4);
+  f12_mul(&t0, &t0, &y5);
+  f12_mul(&t1, &y3, &y5);
+  f12_mul(&t1, &t1, &t0);
+  f12_mul(&t0, &t0, &y2);
+  f12_sqr(&t1, &t1);
+  f12_mul(&t1, &t1, &t0);
+  f12_sqr(&t1, &t1);
+  f12_mul(&t0, &t1, &y1);
+  f12_mul(&t1, &t1, &y0);
+  f12_sqr(&t0, &t0);
+  f12_mul(out, &t0, &t1);
+}
+
+/* ------------------------------------------------------------------ group law */
+static int g1_is_inf(const g1p* a) { return fp_is_zero(&a->z); }
+static void g1_set_inf(g1p* a) { a->x = ONE_M; a->y = ONE_M; memset(&a->z, 0, 32); }
+static void g1_double(g1p* r, const g1p* a) {
+  if (g1_is_inf(a)) { *r = *a; return; }
+  fp A, B, C, D, E, F, t, x3, y3, z3;
+  fp_sqr(&A, &a->x);
+  fp_sqr(&B, &a->y);
+  fp_sqr(&C, &B);
+  fp_add(&t, &a->x, &B);
+  fp_sqr(&D, &t);
+  fp_sub(&D, &D, &A);
+  fp_sub(&D, &D, &C);
+  fp_add(&D, &D, &D);
+  fp_add(&E, &A, &A);
+  fp_add(&E, &E, &A);
+  fp_sqr(&F, &E);
+  fp_add(&t, &D, &D);
+  fp_sub(&x3, &F, &t);
+  fp_add(&t, &C, &C);
+  fp_add(&t, &t, &t);
+  fp_add(&t, &t, &t);
+  fp_sub(&y3, &D, &x3);
+  fp_mul(&y3, &E, &y3);
+  fp_sub(&y3, &y3, &t);
+  fp_mul(&z3, &a->y, &a->z);
+  fp_add(&z3, &z3, &z3);
+  r->x = x3; r->y = y3; r->z = z3;
+}
+static void g1_add(g1p* r, const g1p* a, const g1p* b) {
+  if (g1_is_inf(a)) { *r = *b; return; }
+  if (g1_is_inf(b)) { *r = *a; return; }
+  fp z1z1, z2z2, u1, u2, s1, s2, h, rr, i, j, v, t, x3, y3, z3;
+  fp_sqr(&z1z1, &a->z);
+  fp_sqr(&z2z2, &b->z);
+  fp_mul(&u1, &a->x, &z2z2);
+  fp_mul(&u2, &b->x, &z1z1);
+  fp_mul(&t, &b->z, &z2z2);
+  fp_mul(&s1, &a->y, &t);
+  fp_mul(&t, &a->z, &z1z1);
+  fp_mul(&s2, &b->y, &t);
+  fp_sub(&h, &u2, &u1);
+  fp_sub(&rr, &s2, &s1);
+  if (fp_is_zero(&h)) {
+    if (fp_is_zero(&rr)) { g1_double(r, a); return; }
+    g1_set_inf(r);
+    return;
+  }
+  fp_add(&t, &h, &h);
+  fp_sqr(&i, &t);
+  fp_mul(&j, &h, &i);
+  fp_add(&rr, &rr, &rr);
+  fp_mul(&v, &u1, &i);
+  fp_sqr(&x3, &rr);
+  fp_sub(&x3, &x3, &j);
+  fp_sub(&x3, &x3, &v);
+  fp_sub(&x3, &x3, &v);
+  fp_sub(&t, &v, &x3);
+  fp_mul(&y3, &rr, &t);
+  fp_mul(&t, &s1, &j);
+  fp_add(&t, &t, &t);
+  fp_sub(&y3, &y3, &t);
+  fp_add(&t, &a->z, &b->z);
+  fp_sqr(&t, &t);
+  fp_sub(&t, &t, &z1z1);
+  fp_sub(&t, &t, &z2z2);
+  fp_mul(&z3, &t, &h);
+  r->x = x3; r->y = y3; r->z = z3;
+}
+static void g1_mul(g1p* r, const g1p* a, const uint64_t k[4]) {
+  g1p acc;
+  g1_set_inf(&acc);
+  for (int i = 3; i >= 0; i--)
+    for (int bit = 63; bit >= 0; bit--) {
+      g1_double(&acc, &acc);
+      if ((k[i] >> bit) & 1) g1_add(&acc, &acc, a);
+    }
+  *r = acc;
+}
+static void g1_affine(fp* x, fp* y, const g1p* a) {
+  fp zi, zi2, zi3;
+  fp_inv(&zi, &a->z);
+  fp_sqr(&zi2, &zi);
+  fp_mul(&zi3, &zi2, &zi);
+  fp_mul(x, &a->x, &zi2);
+  fp_mul(y, &a->y, &zi3);
+}
+
+typedef struct { fp2 x, y, z; } g2j;
+static int g2_is_inf(const g2j* a) { return f2_is_zero(&a->z); }
+static void g2_set_inf(g2j* a) { a->x = F2_ONE; a->y = F2_ONE; a->z = F2_ZERO; }
+static void g2_double(g2j* r, const g2j* a) {
+  if (g2_is_inf(a)) { *r = *a; return; }
+  fp2 A, B, C, D, E, F, t, x3, y3, z3;
+  f2_sqr(&A, &a->x);
+  f2_sqr(&B, &a->y);
+  f2_sqr(&C, &B);
+  f2_add(&t, &a->x, &B);
+  f2_sqr(&D, &t);
+  f2_sub(&D, &D, &A);
+  f2_sub(&D, &D, &C);
+  f2_dbl(&D, &D);
+  f2_add(&E, &A, &A);
+  f2_add(&E, &E, &A);
+  f2_sqr(&F, &E);
+  f2_dbl(&t, &D);
+  f2_sub(&x3, &F, &t);
+  f2_dbl(&t, &C);
+  f2_dbl(&t, &t);
+  f2_dbl(&t, &t);
+  f2_sub(&y3, &D, &x3);
+  f2_mul(&y3, &E, &y3);
+  f2_sub(&y3, &y3, &t);
+  f2_mul(&z3, &a->y, &a->z);
+  f2_dbl(&z3, &z3);
+  r->x = x3; r->y = y3; r->z = z3;
+}
+static void g2_add(g2j* r, const g2j* a, const g2j* b) {
+  if (g2_is_inf(a)) { *r = *b; return; }
+  if (g2_is_inf(b)) { *r = *a; return; }
+  fp2 z1z1, z2z2, u1, u2, s1, s2, h, rr, i, j, v, t, x3, y3, z3;
+  f2_sqr(&z1z1, &a->z);
+  f2_sqr(&z2z2, &b->z);
+  f2_mul(&u1, &a->x, &z2z2);
+  f2_mul(&u2, &b->x, &z1z1);
+  f2_mul(&t, &b->z, &z2z2);
+  f2_mul(&s1, &a->y, &t);
+  f2_mul(&t, &a->z, &z1z1);
+  f2_mul(&s2, &b->y, &t);
+  f2_sub(&h, &u2, &u1);
+  f2_sub(&rr, &s2, &s1);
+  if (f2_is_zero(&h)) {
+    if (f2_is_zero(&rr)) { g2_double(r, a); return; }
+    g2_set_inf(r);
+    return;
+  }
+  f2_dbl(&t, &h);
+  f2_sqr(&i, &t);
+  f2_mul(&j, &h, &i);
+  f2_dbl(&rr, &rr);
+  f2_mul(&v, &u1, &i);
+  f2_sqr(&x3, &rr);
+  f2_sub(&x3, &x3, &j);
+  f2_sub(&x3, &x3, &v);
+  f2_sub(&x3, &x3, &v);
+  f2_sub(&t, &v, &x3);
+  f2_mul(&y3, &rr, &t);
+  f2_mul(&t, &s1, &j);
+  f2_dbl(&t, &t);
+  f2_sub(&y3, &y3, &t);
+  f2_add(&t, &a->z, &b->z);
+  f2_sqr(&t, &t);
+  f2_sub(&t, &t, &z1z1);
+  f2_sub(&t, &t, &z2z2);
+  f2_mul(&z3, &t, &h);
+  r->x = x3; r->y = y3; r->z = z3;
+}
+static void g2_mul(g2j* r, const g2j* a, const uint64_t k[4]) {
+  g2j acc;
+  g2_set_inf(&acc);
+  for (int i = 3; i >= 0; i--)
+    for (int bit = 63; bit >= 0; bit--) {
+      g2_double(&acc, &acc);
+      if ((k[i] >> bit) & 1) g2_add(&acc, &acc, a);
+    }
+  *r = acc;
+}
+static void g2_affine(fp2* x, fp2* y, const g2j* a) {
+  fp2 zi, zi2, zi3;
+  f2_inv(&zi, &a->z);
+  f2_sqr(&zi2, &zi);
+  f2_mul(&zi3, &zi2, &zi);
+  f2_mul(x, &a->x, &zi2);
+  f2_mul(y, &a->y, &zi3);
+}
+
+/* ------------------------------------------------------------------ SHA-256 (FIPS 180-4) */
+static const uint32_t SHA_K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+#define ROR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+static void sha_block(uint32_t h[8], const uint8_t* blk) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++)
+    w[i] = ((uint32_t)blk[4 * i] << 24) | ((uint32_t)blk[4 * i + 1] << 16) | ((uint32_t)blk[4 * i + 2] << 8) | blk[4 * i + 3];
+  for (int i = 16; i < 64; i++) {
+    uint32_t s0 = ROR(w[i - 15], 7) ^ ROR(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = ROR(w[i - 2], 17) ^ ROR(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 64; i++) {
+    uint32_t S1 = ROR(e, 6) ^ ROR(e, 11) ^ ROR(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = hh + S1 + ch + SHA_K[i] + w[i];
+    uint32_t S0 = ROR(a, 2) ^ ROR(a, 13) ^ ROR(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+void ref_sha256(const uint8_t* msg, size_t len, uint8_t out[32]) {
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  size_t i = 0;
+  for (; i + 64 <= len; i += 64) sha_block(h, msg + i);
+  uint8_t tail[128];
+  size_t rem = len - i;
+  memset(tail, 0, 128);
+  memcpy(tail, msg + i, rem);
+  tail[rem] = 0x80;
+  size_t tl = (rem + 9 <= 64) ? 64 : 128;
+  uint64_t bits = (uint64_t)len * 8;
+  for (int k = 0; k < 8; k++) tail[tl - 1 - k] = (uint8_t)(bits >> (8 * k));
+  sha_block(h, tail);
+  if (tl == 128) sha_block(h, tail + 64);
+  for (int k = 0; k < 8; k++) {
+    out[4 * k] = (uint8_t)(h[k] >> 24);
+    out[4 * k + 1] = (uint8_t)(h[k] >> 16);
+    out[4 * k + 2] = (uint8_t)(h[k] >> 8);
+    out[4 * k + 3] = (uint8_t)h[k];
+  }
+}
+
+/* ------------------------------------------------------------------ init */
+static void set_dec(fp* r, const char* dec) {
+  /* decimal string -> Montgomery */
+  uint64_t t[4] = {0, 0, 0, 0};
+  for (const char* c = dec; *c; c++) {
+    u128 carry = (uint64_t)(*c - '0');
+    for (int i = 0; i < 4; i++) {
+      u128 v = (u128)t[i] * 10 + carry;
+      t[i] = (uint64_t)v;
+      carry = v >> 64;
+    }
+  }
+  fp_to_mont(r, t);
+}
+static uint64_t ORDER_L[4];
+
+void ref_init(void) {
+  if (g_inited) return;
+  /* PINV = -p^-1 mod 2^64 via Newton */
+  uint64_t inv = 1;
+  for (int i = 0; i < 7; i++) inv *= 2 - P_.v[0] * inv;
+  PINV = (uint64_t)0 - inv;
+  /* R2 = 2^512 mod p: start from 1, double 512 times mod p (plain arithmetic) */
+  uint64_t t[4] = {1, 0, 0, 0};
+  for (int i = 0; i < 512; i++) {
+    uint64_t c = t[3] >> 63;
+    t[3] = (t[3] << 1) | (t[2] >> 63);
+    t[2] = (t[2] << 1) | (t[1] >> 63);
+    t[1] = (t[1] << 1) | (t[0] >> 63);
+    t[0] <<= 1;
+    if (c || fp_geq_p(t)) fp_sub_p(t);
+  }
+  memcpy(R2.v, t, 32);
+  fp one = {{1, 0, 0, 0}};
+  fp_mul(&ONE_M, &one, &R2);
+  memset(&F2_ZERO, 0, sizeof F2_ZERO);
+  F2_ONE.x = F2_ZERO.x;
+  F2_ONE.y = ONE_M;
+  set_dec(&TWIST_B.x, "6500054969564660373279643874235990574282535810762300357187714502686418407178");
+  set_dec(&TWIST_B.y, "45500384786952622612957507119651934019977750675336102500314001518804928850249");
+  fp_from_u64(&CURVE_B, 3);
+  set_dec(&G2X.x, "21167961636542580255011770066570541300993051739349375019639421053990175267184");
+  set_dec(&G2X.y, "64746500191241794695844075326670126197795977525365406531717464316923369116492");
+  set_dec(&G2Y.x, "20666913350058776956210519119118544732556678129809273996262322366050359951122");
+  set_dec(&G2Y.y, "17778617556404439934652658462602675281523610326338642107814333856843981424549");
+  fp_from_u64(&G1X, 1);
+  fp_from_u64(&G1Y, 2);
+  fp_neg(&G1Y, &G1Y);
+  {
+    /* ORDER as plain integer limbs */
+    const char* dec = "65000549695646603732796438742359905742570406053903786389881062969044166799969";
+    uint64_t o[4] = {0, 0, 0, 0};
+    for (const char* c = dec; *c; c++) {
+      u128 carry = (uint64_t)(*c - '0');
+      for (int i = 0; i < 4; i++) {
+        u128 v = (u128)o[i] * 10 + carry;
+        o[i] = (uint64_t)v;
+        carry = v >> 64;
+      }
+    }
+    memcpy(ORDER_L, o, 32);
+  }
+  /* Frobenius constants: gamma1[k] = xi^(k(p-1)/6), gamma2[k] = xi^(k(p^2-1)/6) */
+  fp2 xi;
+  fp_from_u64(&xi.x, 1);
+  fp_from_u64(&xi.y, 3);
+  /* e1 = (p-1)/6 as 4 limbs: compute by long division of p-1 by 6 */
+  uint64_t pm1[4];
+  memcpy(pm1, P_.v, 32);
+  pm1[0] -= 1;
+  uint64_t e1[4];
+  {
+    u128 rem = 0;
+    for (int i = 3; i >= 0; i--) {
+      u128 cur = (rem << 64) | pm1[i];
+      e1[i] = (uint64_t)(cur / 6);
+      rem = cur % 6;
+    }
+  }
+  fp2 g = F2_ONE, base;
+  /* base = xi^((p-1)/6) by square-and-multiply over Fp2 */
+  {
+    fp2 acc = F2_ONE, b = xi;
+    for (int i = 0; i < 4; i++)
+      for (int bit = 0; bit < 64; bit++) {
+        if ((e1[i] >> bit) & 1) f2_mul(&acc, &acc, &b);
+        f2_sqr(&b, &b);
+      }
+    base = acc;
+  }
+  for (int k = 0; k < 6; k++) {
+    GAMMA1[k] = g;
+    f2_mul(&g, &g, &base);
+  }
+  /* gamma2[k] = gamma1[k] * conj(gamma1[k])  (xi^(k(p-1)/6 * (p+1))) */
+  for (int k = 0; k < 6; k++) {
+    fp2 c, r;
+    f2_conj(&c, &GAMMA1[k]);
+    f2_mul(&r, &GAMMA1[k], &c);
+    GAMMA2[k] = r.y;
+  }
+  XI_P13 = GAMMA1[2];  /* xi^((p-1)/3) */
+  XI_P12 = GAMMA1[3];  /* xi^((p-1)/2) */
+  XI_PSQ13 = GAMMA2[2]; /* xi^((p^2-1)/3) */
+  g_inited = 1;
+}
+
+/* ------------------------------------------------------------------ byte codecs (x/crypto + cf) */
+enum { FLAVOR_GO = 0, FLAVOR_CF = 1 };
+enum {
+  RC_OK = 0,
+  RC_SIG_INVALID = 1,
+  RC_HASH_EOF = 2,
+  RC_LEVEL = 3,
+  RC_PK_UNMARSHAL = 4,
+  RC_SIG_UNMARSHAL = 5,
+  RC_EMPTY_AGG = 6,
+  RC_CF_EXCEEDS = 7,
+  RC_CF_MALFORMED = 8,
+  RC_CF_SHORT = 9
+};
+
+/* returns rc; *inf set for the all-zero encoding */
+static int dec_g1(const uint8_t* m, size_t len, int flavor, fp* x, fp* y, int* inf) {
+  uint64_t tx[4], ty[4];
+  if (flavor == FLAVOR_GO ? len != 64 : len < 64) return flavor == FLAVOR_GO ? RC_SIG_UNMARSHAL : RC_CF_SHORT;
+  int gx = int_from_be(tx, m), gy = int_from_be(ty, m + 32);
+  if (flavor == FLAVOR_CF && (gx || gy)) return RC_CF_EXCEEDS;
+  *inf = ((tx[0] | tx[1] | tx[2] | tx[3] | ty[0] | ty[1] | ty[2] | ty[3]) == 0);
+  if (*inf) return RC_OK;
+  fp_to_mont(x, tx);
+  fp_to_mont(y, ty);
+  fp yy, xxx;
+  fp_sqr(&yy, y);
+  fp_sqr(&xxx, x);
+  fp_mul(&xxx, &xxx, x);
+  fp_add(&xxx, &xxx, &CURVE_B);
+  if (!fp_eq(&yy, &xxx)) return flavor == FLAVOR_GO ? RC_SIG_UNMARSHAL : RC_CF_MALFORMED;
+  return RC_OK;
+}
+static int g2_in_subgroup(const fp2* x, const fp2* y) {
+  g2j a = {*x, *y, F2_ONE}, r;
+  g2_mul(&r, &a, ORDER_L);
+  return g2_is_inf(&r);
+}
+static int dec_g2(const uint8_t* m, size_t len, int flavor, fp2* x, fp2* y, int* inf) {
+  uint64_t t[4][4];
+  if (flavor == FLAVOR_GO ? len != 128 : len < 128) return flavor == FLAVOR_GO ? RC_PK_UNMARSHAL : RC_CF_SHORT;
+  int ge = 0, nz = 0;
+  for (int i = 0; i < 4; i++) {
+    ge |= int_from_be(t[i], m + 32 * i);
+    nz |= (t[i][0] | t[i][1] | t[i][2] | t[i][3]) != 0;
+  }
+  if (flavor == FLAVOR_CF && ge) return RC_CF_EXCEEDS;
+  *inf = !nz;
+  if (*inf) return RC_OK;
+  fp_to_mont(&x->x, t[0]);
+  fp_to_mont(&x->y, t[1]);
+  fp_to_mont(&y->x, t[2]);
+  fp_to_mont(&y->y, t[3]);
+  fp2 yy, xxx;
+  f2_sqr(&yy, y);
+  f2_sqr(&xxx, x);
+  f2_mul(&xxx, &xxx, x);
+  f2_add(&xxx, &xxx, &TWIST_B);
+  if (!f2_eq(&yy, &xxx)) return flavor == FLAVOR_GO ? RC_PK_UNMARSHAL : RC_CF_MALFORMED;
+  if (flavor == FLAVOR_CF && !g2_in_subgroup(x, y)) return RC_CF_MALFORMED;
+  return RC_OK;
+}
+static void enc_g1(uint8_t* out, const g1p* a) {
+  if (g1_is_inf(a)) { memset(out, 0, 64); return; }
+  fp x, y;
+  g1_affine(&x, &y, a);
+  fp_to_be(out, &x);
+  fp_to_be(out + 32, &y);
+}
+static void enc_g2(uint8_t* out, const g2j* a) {
+  if (g2_is_inf(a)) { memset(out, 0, 128); return; }
+  fp2 x, y;
+  g2_affine(&x, &y, a);
+  fp_to_be(out, &x.x);
+  fp_to_be(out + 32, &x.y);
+  fp_to_be(out + 64, &y.x);
+  fp_to_be(out + 96, &y.y);
+}
+static void enc_gt(uint8_t* out, const fp12* a) {
+  static const int order[6] = {5, 3, 1, 4, 2, 0};
+  for (int i = 0; i < 6; i++) {
+    fp_to_be(out + 64 * i, &a->c[order[i]].x);
+    fp_to_be(out + 64 * i + 32, &a->c[order[i]].y);
+  }
+}
+
+/* ------------------------------------------------------------------ public entry points */
+/* hashedMessage scalar: returns RC_OK or RC_HASH_EOF */
+int ref_hash_scalar(const uint8_t* msg, size_t len, uint8_t k_be[32]) {
+  uint8_t d[32];
+  ref_sha256(msg, len, d);
+  uint64_t t[4];
+  for (int i = 0; i < 4; i++) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; b++) w = (w << 8) | d[(3 - i) * 8 + b];
+    t[i] = w;
+  }
+  int lt = 0;
+  for (int i = 3; i >= 0; i--) {
+    if (t[i] < ORDER_L[i]) { lt = 1; break; }
+    if (t[i] > ORDER_L[i]) { lt = 0; break; }
+  }
+  if (!lt || (t[0] | t[1] | t[2] | t[3]) == 0) return RC_HASH_EOF;
+  memcpy(k_be, d, 32);
+  return RC_OK;
+}
+static void be_to_limbs(uint64_t t[4], const uint8_t* b) {
+  for (int i = 0; i < 4; i++) {
+    uint64_t w = 0;
+    for (int k = 0; k < 8; k++) w = (w << 8) | b[(3 - i) * 8 + k];
+    t[i] = w;
+  }
+}
+static void hash_point(g1p* h, const uint8_t k_be[32]) {
+  uint64_t k[4];
+  be_to_limbs(k, k_be);
+  g1p g = {G1X, G1Y, ONE_M};
+  g1_mul(h, &g, k);
+}
+
+/* bn256.Pair(g1, g2).Marshal() for marshalled inputs (flavor go) */
+int ref_pair(const uint8_t g1[64], const uint8_t g2[128], uint8_t out[384]) {
+  ref_init();
+  fp px, py;
+  fp2 qx, qy;
+  int i1, i2, rc;
+  if ((rc = dec_g1(g1, 64, FLAVOR_GO, &px, &py, &i1))) return rc;
+  if ((rc = dec_g2(g2, 128, FLAVOR_GO, &qx, &qy, &i2))) return rc;
+  fp12 f, e;
+  if (i1 || i2) {
+    f12_one(&e);
+  } else {
+    miller(&f, &qx, &qy, &px, &py);
+    final_exp(&e, &f);
+  }
+  enc_gt(out, &e);
+  return RC_OK;
+}
+
+/* Reference VerifySignature on decoded points (two pairings, GT compare) */
+static int verify_points(const g1p* hm, int pk_inf, const fp2* qx, const fp2* qy, int sig_inf,
+                         const fp* sx, const fp* sy, int fast) {
+  fp hx, hy;
+  g1_affine(&hx, &hy, hm);
+  fp12 f1, f2_, e1, e2;
+  if (!fast) {
+    if (pk_inf) f12_one(&e1);
+    else { miller(&f1, qx, qy, &hx, &hy); final_exp(&e1, &f1); }
+    if (sig_inf) f12_one(&e2);
+    else { miller(&f2_, &G2X, &G2Y, sx, sy); final_exp(&e2, &f2_); }
+    uint8_t b1[384], b2[384];
+    enc_gt(b1, &e1);
+    enc_gt(b2, &e2);
+    return memcmp(b1, b2, 384) == 0 ? RC_OK : RC_SIG_INVALID;
+  }
+  /* product form: e(H,pk) * conj(f(sig,G2)) then one final exponentiation */
+  fp12 f;
+  f12_one(&f);
+  if (!pk_inf) miller(&f, qx, qy, &hx, &hy);
+  if (!sig_inf) {
+    miller(&f2_, &G2X, &G2Y, sx, sy);
+    f12_conj(&f2_, &f2_);
+    f12_mul(&f, &f, &f2_);
+  }
+  final_exp(&e1, &f);
+  return f12_is_one(&e1) ? RC_OK : RC_SIG_INVALID;
+}
+
+typedef struct {
+  const uint8_t* pks;
+  const uint8_t* sigs;
+  int32_t* codes;
+  size_t begin, end;
+  const g1p* hm;
+  int flavor, fast;
+} vjob;
+
+static void* verify_worker(void* arg) {
+  vjob* j = (vjob*)arg;
+  for (size_t i = j->begin; i < j->end; i++) {
+    fp2 qx, qy;
+    fp sx, sy;
+    int pinf, sinf, rc;
+    rc = dec_g2(j->pks + 128 * i, 128, j->flavor, &qx, &qy, &pinf);
+    if (rc) { j->codes[i] = RC_PK_UNMARSHAL; continue; }
+    rc = dec_g1(j->sigs + 64 * i, 64, j->flavor, &sx, &sy, &sinf);
+    if (rc) { j->codes[i] = RC_SIG_UNMARSHAL; continue; }
+    j->codes[i] = verify_points(j->hm, pinf, &qx, &qy, sinf, &sx, &sy, j->fast);
+  }
+  return 0;
+}
+
+/* n independent PublicKey.VerifySignature(msg, sig) checks; returns count of OK */
+long ref_verify_batch(const uint8_t* msg, size_t msglen, const uint8_t* pks, const uint8_t* sigs,
+                      size_t n, int32_t* codes, int nthreads, int flavor, int fast) {
+  ref_init();
+  uint8_t k[32];
+  if (ref_hash_scalar(msg, msglen, k) != RC_OK) {
+    for (size_t i = 0; i < n; i++) codes[i] = RC_HASH_EOF;
+    return 0;
+  }
+  g1p hm;
+  hash_point(&hm, k);
+  if (nthreads < 1) nthreads = 1;
+  if ((size_t)nthreads > n && n > 0) nthreads = (int)n;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  vjob* jobs = (vjob*)malloc(sizeof(vjob) * nthreads);
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (vjob){pks, sigs, codes, n * t / nthreads, n * (t + 1) / nthreads, &hm, flavor, fast};
+    pthread_create(&th[t], 0, verify_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], 0);
+  free(th);
+  free(jobs);
+  long ok = 0;
+  for (size_t i = 0; i < n; i++) ok += codes[i] == RC_OK;
+  return ok;
+}
+
+/* Aggregated requests over a registry (processing.go verifySignature):
+ * request r covers registry[off[r], off[r]+bitlen[r]) with its bitset words
+ * at words + woff[r] (willf layout), signature sigs + 64r. level_len[r] is the
+ * partitioner's level size; bitlen != level_len -> RC_LEVEL. agg_out (nullable)
+ * receives the 128-byte marshal of the aggregate key. */
+typedef struct {
+  const uint8_t* reg;
+  size_t nreg;
+  const uint32_t *off, *bitlen, *level_len;
+  const uint64_t* words;
+  const uint64_t* woff;
+  const uint8_t* sigs;
+  int32_t* codes;
+  uint8_t* agg_out;
+  size_t begin, end;
+  const g1p* hm;
+  int fast;
+} ajob;
+
+static void* agg_worker(void* arg) {
+  ajob* j = (ajob*)arg;
+  for (size_t r = j->begin; r < j->end; r++) {
+    uint32_t bl = j->bitlen[r];
+    if (bl != j->level_len[r] || (size_t)j->off[r] + bl > j->nreg) { j->codes[r] = RC_LEVEL; continue; }
+    g2j acc;
+    g2_set_inf(&acc);
+    int any = 0, bad = 0;
+    for (uint32_t i = 0; i < bl; i++) {
+      uint64_t w = j->words[j->woff[r] + (i >> 6)];
+      if (!((w >> (i & 63)) & 1)) continue;
+      fp2 x, y;
+      int inf;
+      if (dec_g2(j->reg + 128 * ((size_t)j->off[r] + i), 128, FLAVOR_GO, &x, &y, &inf)) { bad = 1; break; }
+      g2j pt;
+      if (inf) g2_set_inf(&pt);
+      else { pt.x = x; pt.y = y; pt.z = F2_ONE; }
+      g2_add(&acc, &acc, &pt);
+      any = 1;
+    }
+    if (bad) { j->codes[r] = RC_PK_UNMARSHAL; continue; }
+    if (j->agg_out) enc_g2(j->agg_out + 128 * r, &acc);
+    if (!any) { j->codes[r] = RC_EMPTY_AGG; continue; }
+    fp sx, sy;
+    int sinf;
+    if (dec_g1(j->sigs + 64 * r, 64, FLAVOR_GO, &sx, &sy, &sinf)) { j->codes[r] = RC_SIG_UNMARSHAL; continue; }
+    fp2 qx = F2_ZERO, qy = F2_ZERO;
+    int pinf = g2_is_inf(&acc);
+    if (!pinf) g2_affine(&qx, &qy, &acc);
+    j->codes[r] = verify_points(j->hm, pinf, &qx, &qy, sinf, &sx, &sy, j->fast);
+  }
+  return 0;
+}
+
+long ref_verify_aggregate(const uint8_t* msg, size_t msglen, const uint8_t* reg, size_t nreg,
+                          size_t nreq, const uint32_t* off, const uint32_t* bitlen,
+                          const uint32_t* level_len, const uint64_t* words, const uint64_t* woff,
+                          const uint8_t* sigs, int32_t* codes, uint8_t* agg_out, int nthreads,
+                          int fast) {
+  ref_init();
+  uint8_t k[32];
+  int hash_ok = ref_hash_scalar(msg, msglen, k) == RC_OK;
+  g1p hm;
+  if (hash_ok) hash_point(&hm, k);
+  if (nthreads < 1) nthreads = 1;
+  if ((size_t)nthreads > nreq && nreq > 0) nthreads = (int)nreq;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  ajob* jobs = (ajob*)malloc(sizeof(ajob) * nthreads);
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (ajob){reg, nreg, off, bitlen, level_len, words, woff, sigs, codes, agg_out,
+                     nreq * t / nthreads, nreq * (t + 1) / nthreads, &hm, fast};
+    pthread_create(&th[t], 0, agg_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], 0);
+  free(th);
+  free(jobs);
+  long ok = 0;
+  for (size_t r = 0; r < nreq; r++) {
+    if (!hash_ok && codes[r] == RC_OK) codes[r] = RC_HASH_EOF;
+    if (!hash_ok && codes[r] == RC_SIG_INVALID) codes[r] = RC_HASH_EOF;
+    ok += codes[r] == RC_OK;
+  }
+  return ok;
+}
+
+/* ---- fixture helpers: keygen from a 32-byte-per-try scalar list, signing, combine ---- */
+/* pk = k * G2 for big-endian scalars k (n x 32 bytes) */
+void ref_g2_scalar_base(const uint8_t* k_be, size_t n, uint8_t* out) {
+  ref_init();
+  g2j g = {G2X, G2Y, F2_ONE};
+  for (size_t i = 0; i < n; i++) {
+    uint64_t k[4];
+    be_to_limbs(k, k_be + 32 * i);
+    g2j r;
+    g2_mul(&r, &g, k);
+    enc_g2(out + 128 * i, &r);
+  }
+}
+/* sig = k * H(msg) ; returns RC_HASH_EOF if the message cannot be hashed */
+int ref_sign(const uint8_t* msg, size_t msglen, const uint8_t* k_be, size_t n, uint8_t* out) {
+  ref_init();
+  uint8_t hk[32];
+  if (ref_hash_scalar(msg, msglen, hk) != RC_OK) return RC_HASH_EOF;
+  g1p hm;
+  hash_point(&hm, hk);
+  for (size_t i = 0; i < n; i++) {
+    uint64_t k[4];
+    be_to_limbs(k, k_be + 32 * i);
+    g1p r;
+    g1_mul(&r, &hm, k);
+    enc_g1(out + 64 * i, &r);
+  }
+  return RC_OK;
+}
+/* out = a + b for marshalled points (G1: w = 64, G2: w = 128) */
+int ref_g1_add(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  ref_init();
+  fp x, y;
+  int inf, rc;
+  g1p pa, pb, r;
+  if ((rc = dec_g1(a, 64, FLAVOR_GO, &x, &y, &inf))) return rc;
+  if (inf) g1_set_inf(&pa); else { pa.x = x; pa.y = y; pa.z = ONE_M; }
+  if ((rc = dec_g1(b, 64, FLAVOR_GO, &x, &y, &inf))) return rc;
+  if (inf) g1_set_inf(&pb); else { pb.x = x; pb.y = y; pb.z = ONE_M; }
+  g1_add(&r, &pa, &pb);
+  enc_g1(out, &r);
+  return RC_OK;
+}
+int ref_g2_add(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  ref_init();
+  fp2 x, y;
+  int inf, rc;
+  g2j pa, pb, r;
+  if ((rc = dec_g2(a, 128, FLAVOR_GO, &x, &y, &inf))) return rc;
+  if (inf) g2_set_inf(&pa); else { pa.x = x; pa.y = y; pa.z = F2_ONE; }
+  if ((rc = dec_g2(b, 128, FLAVOR_GO, &x, &y, &inf))) return rc;
+  if (inf) g2_set_inf(&pb); else { pb.x = x; pb.y = y; pb.z = F2_ONE; }
+  g2_add(&r, &pa, &pb);
+  enc_g2(out, &r);
+  return RC_OK;
+}
+int ref_decode_g2(const uint8_t* m, size_t len, int flavor) {
+  ref_init();
+  fp2 x, y;
+  int inf;
+  return dec_g2(m, len, flavor, &x, &y, &inf);
+}
+int ref_decode_g1(const uint8_t* m, size_t len, int flavor) {
+  ref_init();
+  fp x, y;
+  int inf;
+  return dec_g1(m, len, flavor, &x, &y, &inf);
+}
