@@ -1,0 +1,86 @@
+"""ctypes binding of include/handel_gpu.h (libhandel_gpu.so, built in-tree).
+
+There is no CPU fallback: if the HIP library is missing or fails to load,
+every entry point raises. The oracle under oracle/ is never imported here.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import build as _build
+
+_lock = threading.Lock()
+_lib = None
+
+# hg_code values (include/handel_gpu.h)
+HG_OK = 0
+HG_ERR_SIG_INVALID = 1
+HG_ERR_HASH_EOF = 2
+HG_ERR_LEVEL = 3
+HG_ERR_PK_UNMARSHAL = 4
+HG_ERR_SIG_UNMARSHAL = 5
+HG_ERR_EMPTY_AGG = 6
+HG_ERR_CF_EXCEEDS = 7
+HG_ERR_CF_MALFORMED = 8
+HG_ERR_CF_SHORT = 9
+HG_ERR_ARG = 100
+HG_ERR_DEVICE = 101
+
+HG_FLAVOR_GO = 0
+HG_FLAVOR_CF = 1
+
+# every symbol include/handel_gpu.h declares: name -> (restype, argtypes)
+_P = ctypes.c_void_p
+_SZ = ctypes.c_size_t
+_I = ctypes.c_int
+SIGNATURES = {
+    "hg_version": (_I, []),
+    "hg_create": (_I, [_I, _I, ctypes.POINTER(_P)]),
+    "hg_destroy": (None, [_P]),
+    "hg_last_error": (ctypes.c_char_p, [_P]),
+    "hg_code_string": (ctypes.c_char_p, [_I, _I]),
+    "hg_registry_load": (_I, [_P, _P, _SZ, _P]),
+    "hg_registry_size": (_SZ, [_P]),
+    "hg_set_message": (_I, [_P, _P, _SZ]),
+    "hg_verify_batch": (_I, [_P, _P, _P, _SZ, _P]),
+    "hg_verify_batch_device": (_I, [_P, _P, _P, _SZ, _P, _P]),
+    "hg_verify_aggregate": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P, _P]),
+    "hg_verify_aggregate_device": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
+    "hg_aggregate_pk": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P]),
+    "hg_combine_g1": (_I, [_P, _P, _P, _SZ, _P, _P]),
+    "hg_pair": (_I, [_P, _P, _P, _SZ, _P, _P]),
+    "hg_keygen": (_I, [_P, _P, _SZ, _P]),
+    "hg_sign": (_I, [_P, _P, _SZ, _P]),
+    "hg_debug_fp_mul": (_I, [_P, _P, _P, _SZ, _P]),
+    "hg_sync": (_I, [_P]),
+}
+
+
+class HandelGPUError(RuntimeError):
+    pass
+
+
+def load(build_if_missing: bool = True):
+    """Loads (building first if needed) the HIP library; raises on failure."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = _build.LIB
+        if not os.path.exists(path):
+            if not build_if_missing:
+                raise HandelGPUError(f"HIP library not built: {path}")
+            _build.build_library()
+        try:
+            L = ctypes.CDLL(path)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise HandelGPUError(f"cannot load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)  # AttributeError = missing export: fail loudly
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+        return L

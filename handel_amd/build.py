@@ -1,0 +1,66 @@
+"""Builds the in-tree HIP library handel_amd/_build/libhandel_gpu.so.
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU
+container (``__graft_entry__.build()``) and the resulting .so travels to the
+GPU box with the repo snapshot.
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT_DIR = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT_DIR, "libhandel_gpu.so")
+SOURCES = ["bn256_kernels.hip", "hg_api.cpp"]
+HEADERS = ["bn256_fp.h", "bn256_curve.h", "bn256_team.h", "bn256_kernels.h", "bn256_constants.h"]
+ARCH = os.environ.get("HG_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def _inputs():
+    files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    files.append(os.path.join(HERE, "..", "include", "handel_gpu.h"))
+    files.append(os.path.abspath(__file__))
+    return files
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(f) <= t for f in _inputs())
+
+
+def build_library(force: bool = False, verbose: bool = True) -> str:
+    if not force and up_to_date():
+        return LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+
+    def compile_one(src):
+        obj = os.path.join(OUT_DIR, os.path.splitext(src)[0] + ".o")
+        cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build_library(force="--force" in sys.argv)
+    print(LIB)

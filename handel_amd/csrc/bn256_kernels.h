@@ -1,0 +1,54 @@
+// bn256_kernels.h — device data layout shared by the kernels and the host API.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/handel_gpu.h"
+#include "bn256_fp.h"
+
+namespace hg {
+
+// Decoded points in HBM: affine, Montgomery form, explicit infinity flag.
+struct PointG1 {
+  Fp x, y;
+  uint32_t inf;
+  uint32_t pad[3];
+};
+struct PointG2 {
+  Fp2 x, y;
+  uint32_t inf;
+  uint32_t pad[3];
+};
+// One pairing check: e(H, pk) * e(-sig, G2Base) == 1
+struct CheckIn {
+  PointG2 pk;
+  PointG1 sig;
+};
+// A G2Base Miller-loop line: value c + b w + a w^3 with b = bx * Px, c = cy * Py
+struct LineCoef {
+  Fp2 a, bx, cy;
+};
+static constexpr int kNumLines = 65 + 18 + 2;  // doublings + NAF additions + 2 Frobenius lines
+
+using AggRequest = hg_request;
+
+void launch_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int32_t* codes, hipStream_t s);
+void launch_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes, hipStream_t s);
+void launch_encode_g2(const PointG2* in, int n, uint8_t* out, hipStream_t s);
+void launch_encode_g1(const PointG1* in, int n, uint8_t* out, hipStream_t s);
+void launch_g2_mul_base(const uint8_t* scalars, int n, PointG2* out, hipStream_t s);
+void launch_g1_mul(const PointG1* base, const uint8_t* scalars, int n, PointG1* out, hipStream_t s);
+void launch_hash_point(const uint32_t* k, PointG1* out, hipStream_t s);
+void launch_g2_lines(LineCoef* tab, hipStream_t s);
+void launch_verify(const CheckIn* in, int n, const LineCoef* tab, const PointG1* h, int32_t* codes, hipStream_t s);
+void launch_pair(const PointG1* g1s, const PointG2* g2s, int n, const LineCoef* tab, uint8_t* gt, hipStream_t s);
+void launch_aggregate(const PointG2* reg, int nreg, const AggRequest* reqs, int n, const uint64_t* words,
+                      CheckIn* out, int32_t* codes, hipStream_t s);
+void launch_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t* out, hipStream_t s);
+void launch_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, CheckIn* out, hipStream_t s);
+void launch_merge_codes(const int32_t* a, const int32_t* b, int n, int32_t* out, hipStream_t s);
+void launch_sig_into_checks(const PointG1* sigs, int n, CheckIn* out, hipStream_t s);
+void launch_extract_pk(const CheckIn* in, int n, PointG2* out, hipStream_t s);
+void launch_fp_mul(const uint32_t* a, const uint32_t* b, int n, uint32_t* out, hipStream_t s);
+
+}  // namespace hg

@@ -1,0 +1,588 @@
+// hg_api.cpp — host side of the C ABI declared in include/handel_gpu.h.
+//
+// Owns the HIP resources of one verification context and sequences the
+// kernels of bn256_kernels.hip. Mirrors the reference's call structure:
+//   Constructor / G2Base           -> hg_create (+ the G2Base line table)
+//   registry PublicKey.Unmarshal   -> hg_registry_load (simul/lib/nodes.go:44-64)
+//   hashedMessage                  -> hg_set_message (once per message)
+//   PublicKey.VerifySignature      -> hg_verify_batch
+//   processing.go verifySignature  -> hg_verify_aggregate
+// Error precedence follows the order in which the reference surfaces errors:
+// unmarshal (at parse time) > bitset/level check > hashedMessage EOF >
+// nil-aggregate panic > pairing verdict.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bn256_kernels.h"
+
+using namespace hg;
+
+namespace {
+
+// ------------------------------------------------------------ SHA-256 (FIPS 180-4)
+const uint32_t kSha[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+void sha256_block(uint32_t h[8], const uint8_t* b) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++)
+    w[i] = (uint32_t)b[4 * i] << 24 | (uint32_t)b[4 * i + 1] << 16 | (uint32_t)b[4 * i + 2] << 8 | b[4 * i + 3];
+  for (int i = 16; i < 64; i++) {
+    uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = h[0], bb = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 64; i++) {
+    uint32_t t1 = hh + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + kSha[i] + w[i];
+    uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & bb) ^ (a & c) ^ (bb & c));
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = bb;
+    bb = a;
+    a = t1 + t2;
+  }
+  h[0] += a; h[1] += bb; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+void sha256(const uint8_t* m, size_t len, uint8_t out[32]) {
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  size_t i = 0;
+  for (; i + 64 <= len; i += 64) sha256_block(h, m + i);
+  uint8_t tail[128] = {0};
+  size_t rem = len - i;
+  if (rem) memcpy(tail, m + i, rem);
+  tail[rem] = 0x80;
+  size_t tl = rem + 9 <= 64 ? 64 : 128;
+  uint64_t bits = (uint64_t)len * 8;
+  for (int k = 0; k < 8; k++) tail[tl - 1 - k] = (uint8_t)(bits >> (8 * k));
+  sha256_block(h, tail);
+  if (tl == 128) sha256_block(h, tail + 64);
+  for (int k = 0; k < 8; k++) {
+    out[4 * k] = (uint8_t)(h[k] >> 24);
+    out[4 * k + 1] = (uint8_t)(h[k] >> 16);
+    out[4 * k + 2] = (uint8_t)(h[k] >> 8);
+    out[4 * k + 3] = (uint8_t)h[k];
+  }
+}
+
+const uint32_t kOrder32[8] = {HG_ORDER32};
+
+// crypto/rand.Int(bytes.NewBuffer(d), Order) as used by hashedMessage: the
+// single 32-byte read is accepted iff 0 < int(d) < n; otherwise the next
+// read hits EOF.
+bool hash_scalar(const uint8_t d[32], uint32_t k[8]) {
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = d + (7 - i) * 4;
+    k[i] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
+  }
+  bool zero = true;
+  for (int i = 0; i < 8; i++) zero &= k[i] == 0;
+  if (zero) return false;
+  for (int i = 7; i >= 0; i--) {
+    if (k[i] < kOrder32[i]) return true;
+    if (k[i] > kOrder32[i]) return false;
+  }
+  return false;  // equal to n
+}
+
+__global__ void k_fill_codes(int32_t* c, int n, int32_t from, int32_t to) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && c[i] == from) c[i] = to;
+}
+// final = sig decode error > level error > hash EOF > empty aggregate > (verify)
+__global__ void k_agg_codes(const int32_t* sig_codes, const int32_t* lvl_codes, int hash_eof, int n, int32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t c = sig_codes[i];
+  if (c == HG_OK && lvl_codes[i] == HG_ERR_LEVEL) c = HG_ERR_LEVEL;
+  if (c == HG_OK && hash_eof) c = HG_ERR_HASH_EOF;
+  if (c == HG_OK) c = lvl_codes[i];
+  out[i] = c;
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n < 64 ? 64 : n;
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct hg_ctx {
+  int device = 0;
+  int flavor = HG_FLAVOR_GO;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  // constant tables
+  LineCoef* d_lines = nullptr;
+  PointG1* d_h = nullptr;
+  uint32_t* d_k = nullptr;
+  bool has_msg = false;
+  bool hash_eof = false;
+  // registry
+  DevBuf<PointG2> reg;
+  size_t nreg = 0;
+  // workspaces
+  DevBuf<uint8_t> bytes_a, bytes_b;
+  DevBuf<PointG2> pts2;
+  DevBuf<PointG1> pts1, pts1b;
+  DevBuf<CheckIn> checks;
+  DevBuf<int32_t> codes_a, codes_b, codes_c;
+  DevBuf<hg_request> reqs;
+  DevBuf<uint64_t> words;
+};
+
+#define HG_CHECK(ctx, expr)                                                        \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return HG_ERR_DEVICE;                                                        \
+    }                                                                              \
+  } while (0)
+
+static int nb(size_t n) { return (int)((n + 255) / 256); }
+
+static int check_launch(hg_ctx* c) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    c->err = std::string("kernel launch: ") + hipGetErrorString(e);
+    return HG_ERR_DEVICE;
+  }
+  return HG_OK;
+}
+
+extern "C" {
+
+int hg_version(void) { return 1; }
+
+const char* hg_code_string(int code, int flavor) {
+  switch (code) {
+    case HG_OK: return "";
+    case HG_ERR_SIG_INVALID: return "bn256: signature invalid";
+    case HG_ERR_HASH_EOF: return "EOF";
+    case HG_ERR_LEVEL: return "handel: inconsistent bitset with given level";
+    case HG_ERR_PK_UNMARSHAL: return "unable to unmarshal";
+    case HG_ERR_SIG_UNMARSHAL: return flavor == HG_FLAVOR_CF ? "bn256: multisig can't unmarshal: bn256: malformed point"
+                                                             : "bn256: multisig can't unmarshal";
+    case HG_ERR_EMPTY_AGG: return "runtime error: invalid memory address or nil pointer dereference";
+    case HG_ERR_CF_EXCEEDS: return "bn256: coordinate exceeds modulus";
+    case HG_ERR_CF_MALFORMED: return "bn256: malformed point";
+    case HG_ERR_CF_SHORT: return "bn256: not enough data";
+    case HG_ERR_ARG: return "invalid argument";
+    default: return "device error";
+  }
+}
+
+const char* hg_last_error(hg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int hg_create(int device, int flavor, hg_ctx** out) {
+  if (!out || (flavor != HG_FLAVOR_GO && flavor != HG_FLAVOR_CF)) return HG_ERR_ARG;
+  *out = nullptr;
+  hg_ctx* c = new hg_ctx();
+  c->device = device;
+  c->flavor = flavor;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->d_lines, sizeof(LineCoef) * kNumLines);
+  if (e == hipSuccess) e = hipMalloc(&c->d_h, sizeof(PointG1));
+  if (e == hipSuccess) e = hipMalloc(&c->d_k, sizeof(uint32_t) * 8);
+  if (e != hipSuccess) {
+    fprintf(stderr, "hg_create: %s\n", hipGetErrorString(e));
+    delete c;
+    return HG_ERR_DEVICE;
+  }
+  launch_g2_lines(c->d_lines, c->stream);
+  if (check_launch(c) != HG_OK || hipStreamSynchronize(c->stream) != hipSuccess) {
+    fprintf(stderr, "hg_create: %s\n", c->err.c_str());
+    delete c;
+    return HG_ERR_DEVICE;
+  }
+  *out = c;
+  return HG_OK;
+}
+
+void hg_destroy(hg_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->reg.release();
+  c->bytes_a.release();
+  c->bytes_b.release();
+  c->pts2.release();
+  c->pts1.release();
+  c->pts1b.release();
+  c->checks.release();
+  c->codes_a.release();
+  c->codes_b.release();
+  c->codes_c.release();
+  c->reqs.release();
+  c->words.release();
+  if (c->d_lines) (void)hipFree(c->d_lines);
+  if (c->d_h) (void)hipFree(c->d_h);
+  if (c->d_k) (void)hipFree(c->d_k);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int hg_sync(hg_ctx* c) {
+  if (!c) return HG_ERR_ARG;
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_set_message(hg_ctx* c, const uint8_t* msg, size_t len) {
+  if (!c || (!msg && len)) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  uint8_t d[32];
+  sha256(msg, len, d);
+  uint32_t k[8];
+  c->has_msg = true;
+  c->hash_eof = !hash_scalar(d, k);
+  if (c->hash_eof) return HG_ERR_HASH_EOF;
+  HG_CHECK(c, hipMemcpyAsync(c->d_k, k, sizeof k, hipMemcpyHostToDevice, c->stream));
+  launch_hash_point(c->d_k, c->d_h, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
+  if (!c || (!pks && n)) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->reg.ensure(n));
+  HG_CHECK(c, c->bytes_a.ensure(n * 128));
+  HG_CHECK(c, c->codes_a.ensure(n));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, pks, n * 128, hipMemcpyHostToDevice, c->stream));
+  launch_decode_g2(c->bytes_a.p, (int)n, c->flavor, c->reg.p, c->codes_a.p, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  std::vector<int32_t> h(n);
+  if (n) HG_CHECK(c, hipMemcpyAsync(h.data(), c->codes_a.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  int bad = 0;
+  for (size_t i = 0; i < n; i++) bad |= h[i] != HG_OK;
+  if (codes && n) memcpy(codes, h.data(), n * 4);
+  c->nreg = n;
+  if (bad) {
+    c->err = "registry contains keys that fail to unmarshal";
+    return HG_ERR_PK_UNMARSHAL;
+  }
+  return HG_OK;
+}
+
+size_t hg_registry_size(hg_ctx* c) { return c ? c->nreg : 0; }
+
+static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n,
+                                      int32_t* d_codes, hipStream_t s) {
+  if (!c->has_msg) {
+    c->err = "hg_set_message was not called";
+    return HG_ERR_ARG;
+  }
+  HG_CHECK(c, c->pts2.ensure(n));
+  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, c->checks.ensure(n));
+  HG_CHECK(c, c->codes_a.ensure(n));
+  HG_CHECK(c, c->codes_b.ensure(n));
+  launch_decode_g2(d_pks, (int)n, c->flavor, c->pts2.p, c->codes_a.p, s);
+  launch_decode_g1(d_sigs, (int)n, c->flavor, c->pts1.p, c->codes_b.p, s);
+  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, d_codes, s);
+  if (c->hash_eof) {
+    k_fill_codes<<<nb(n), 256, 0, s>>>(d_codes, (int)n, HG_OK, HG_ERR_HASH_EOF);
+    return check_launch(c);
+  }
+  launch_checks_from_points(c->pts2.p, c->pts1.p, (int)n, c->checks.p, s);
+  launch_verify(c->checks.p, (int)n, c->d_lines, c->d_h, d_codes, s);
+  return check_launch(c);
+}
+
+int hg_verify_batch_device(hg_ctx* c, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n, int32_t* d_codes,
+                           void* stream) {
+  if (!c || (n && (!d_pks || !d_sigs || !d_codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return verify_batch_device_locked(c, d_pks, d_sigs, n, d_codes, s);
+}
+
+int hg_verify_batch(hg_ctx* c, const uint8_t* pks, const uint8_t* sigs, size_t n, int32_t* codes) {
+  if (!c || (n && (!pks || !sigs || !codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 128));
+  HG_CHECK(c, c->bytes_b.ensure(n * 64));
+  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, pks, n * 128, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
+  int rc = verify_batch_device_locked(c, c->bytes_a.p, c->bytes_b.p, n, c->codes_c.p, c->stream);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+// host-side request validation: the level check of processing.go:350-352
+static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector<int32_t>& out, bool* range_ok) {
+  out.resize(n);
+  *range_ok = true;
+  for (size_t i = 0; i < n; i++) {
+    const hg_request& r = reqs[i];
+    bool ok = r.bitlen == r.level_size && (size_t)r.offset + r.bitlen <= c->nreg;
+    out[i] = ok ? HG_OK : HG_ERR_LEVEL;
+  }
+}
+
+static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                                   const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
+                                   bool verify, hipStream_t s) {
+  HG_CHECK(c, c->checks.ensure(n));
+  launch_aggregate(c->reg.p, (int)c->nreg, d_reqs, (int)n, d_words, c->checks.p, d_lvl, s);
+  if (d_agg) {
+    HG_CHECK(c, c->pts2.ensure(n));
+    launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);
+    launch_encode_g2(c->pts2.p, (int)n, d_agg, s);
+  }
+  if (!verify) return check_launch(c);
+  if (!c->has_msg) {
+    c->err = "hg_set_message was not called";
+    return HG_ERR_ARG;
+  }
+  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, c->codes_b.ensure(n));
+  launch_decode_g1(d_sigs, (int)n, c->flavor, c->pts1.p, c->codes_b.p, s);
+  k_agg_codes<<<nb(n), 256, 0, s>>>(c->codes_b.p, d_lvl, c->hash_eof ? 1 : 0, (int)n, d_codes);
+  if (!c->hash_eof) {
+    launch_sig_into_checks(c->pts1.p, (int)n, c->checks.p, s);
+    launch_verify(c->checks.p, (int)n, c->d_lines, c->d_h, d_codes, s);
+  }
+  return check_launch(c);
+}
+
+__global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool ok = r[i].bitlen == r[i].level_size && (uint64_t)r[i].offset + r[i].bitlen <= nreg;
+  out[i] = ok ? HG_OK : HG_ERR_LEVEL;
+}
+
+int hg_verify_aggregate_device(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                               const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg_pk_out, void* stream) {
+  if (!c || (n && (!d_reqs || !d_sigs || !d_codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  HG_CHECK(c, c->codes_c.ensure(n));
+  k_level_codes<<<nb(n), 256, 0, s>>>(d_reqs, (int)n, (uint32_t)c->nreg, c->codes_c.p);
+  return aggregate_device_locked(c, d_reqs, n, d_words, d_sigs, d_codes, d_agg_pk_out, c->codes_c.p, true, s);
+}
+
+static int aggregate_host(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
+                          const uint8_t* sigs, int32_t* codes, uint8_t* agg_out, bool verify) {
+  std::vector<int32_t> lvl;
+  bool range_ok;
+  level_codes(c, reqs, n, lvl, &range_ok);
+  for (size_t i = 0; i < n; i++) {
+    if (lvl[i] == HG_OK && (size_t)reqs[i].word_offset + (reqs[i].bitlen + 63) / 64 > nwords) {
+      c->err = "request words out of range";
+      return HG_ERR_ARG;
+    }
+  }
+  HG_CHECK(c, c->reqs.ensure(n));
+  HG_CHECK(c, c->words.ensure(nwords ? nwords : 1));
+  HG_CHECK(c, c->codes_a.ensure(n));
+  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, hipMemcpyAsync(c->reqs.p, reqs, n * sizeof(hg_request), hipMemcpyHostToDevice, c->stream));
+  if (nwords) HG_CHECK(c, hipMemcpyAsync(c->words.p, words, nwords * 8, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->codes_c.p, lvl.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  uint8_t* d_agg = nullptr;
+  if (agg_out) {
+    HG_CHECK(c, c->bytes_a.ensure(n * 128));
+    d_agg = c->bytes_a.p;
+  }
+  if (verify) {
+    HG_CHECK(c, c->bytes_b.ensure(n * 64));
+    HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
+  }
+  int rc = aggregate_device_locked(c, c->reqs.p, n, c->words.p, verify ? c->bytes_b.p : nullptr, c->codes_a.p, d_agg,
+                                   c->codes_c.p, verify, c->stream);
+  if (rc) return rc;
+  if (agg_out) HG_CHECK(c, hipMemcpyAsync(agg_out, d_agg, n * 128, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, verify ? c->codes_a.p : c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  if (agg_out) {
+    // the reference has no aggregate for level errors / empty bitsets: zero them
+    for (size_t i = 0; i < n; i++)
+      if (lvl[i] != HG_OK || codes[i] == HG_ERR_EMPTY_AGG) memset(agg_out + 128 * i, 0, 128);
+  }
+  return HG_OK;
+}
+
+int hg_verify_aggregate(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
+                        const uint8_t* sigs, int32_t* codes, uint8_t* agg_pk_out) {
+  if (!c || (n && (!reqs || !sigs || !codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  return aggregate_host(c, reqs, n, words, nwords, sigs, codes, agg_pk_out, true);
+}
+
+int hg_aggregate_pk(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
+                    uint8_t* agg_pk_out, int32_t* codes) {
+  if (!c || (n && (!reqs || !agg_pk_out || !codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  return aggregate_host(c, reqs, n, words, nwords, nullptr, codes, agg_pk_out, false);
+}
+
+int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out, int32_t* codes) {
+  if (!c || (n && (!a || !b || !out || !codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 64));
+  HG_CHECK(c, c->bytes_b.ensure(n * 64));
+  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, c->pts1b.ensure(n));
+  HG_CHECK(c, c->codes_a.ensure(n));
+  HG_CHECK(c, c->codes_b.ensure(n));
+  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, a, n * 64, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, b, n * 64, hipMemcpyHostToDevice, c->stream));
+  launch_decode_g1(c->bytes_a.p, (int)n, c->flavor, c->pts1.p, c->codes_a.p, c->stream);
+  launch_decode_g1(c->bytes_b.p, (int)n, c->flavor, c->pts1b.p, c->codes_b.p, c->stream);
+  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, c->codes_c.p, c->stream);
+  launch_g1_combine(c->pts1.p, c->pts1b.p, (int)n, c->bytes_a.p, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_pair(hg_ctx* c, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t* gt_out, int32_t* codes) {
+  if (!c || (n && (!g1s || !g2s || !gt_out || !codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 128 > n * 384 ? n * 128 : n * 384));
+  HG_CHECK(c, c->bytes_b.ensure(n * 64));
+  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, c->pts2.ensure(n));
+  HG_CHECK(c, c->codes_a.ensure(n));
+  HG_CHECK(c, c->codes_b.ensure(n));
+  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, g2s, n * 128, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, g1s, n * 64, hipMemcpyHostToDevice, c->stream));
+  launch_decode_g2(c->bytes_a.p, (int)n, HG_FLAVOR_GO, c->pts2.p, c->codes_a.p, c->stream);
+  launch_decode_g1(c->bytes_b.p, (int)n, HG_FLAVOR_GO, c->pts1.p, c->codes_b.p, c->stream);
+  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, c->codes_c.p, c->stream);
+  launch_pair(c->pts1.p, c->pts2.p, (int)n, c->d_lines, c->bytes_a.p, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(gt_out, c->bytes_a.p, n * 384, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_keygen(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* pks_out) {
+  if (!c || (n && (!scalars_be || !pks_out))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 128));
+  HG_CHECK(c, c->bytes_b.ensure(n * 32));
+  HG_CHECK(c, c->pts2.ensure(n));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
+  launch_g2_mul_base(c->bytes_b.p, (int)n, c->pts2.p, c->stream);
+  launch_encode_g2(c->pts2.p, (int)n, c->bytes_a.p, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(pks_out, c->bytes_a.p, n * 128, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_sign(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out) {
+  if (!c || (n && (!scalars_be || !sigs_out))) return HG_ERR_ARG;
+  if (!c->has_msg) {
+    c->err = "hg_set_message was not called";
+    return HG_ERR_ARG;
+  }
+  if (c->hash_eof) return HG_ERR_HASH_EOF;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 64));
+  HG_CHECK(c, c->bytes_b.ensure(n * 32));
+  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
+  launch_g1_mul(c->d_h, c->bytes_b.p, (int)n, c->pts1.p, c->stream);
+  launch_encode_g1(c->pts1.p, (int)n, c->bytes_a.p, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(sigs_out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_debug_fp_mul(hg_ctx* c, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out) {
+  if (!c || (n && (!a || !b || !out))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 32 * 3));
+  uint32_t* da = (uint32_t*)c->bytes_a.p;
+  HG_CHECK(c, hipMemcpyAsync(da, a, n * 32, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(da + 8 * n, b, n * 32, hipMemcpyHostToDevice, c->stream));
+  launch_fp_mul(da, da + 8 * n, (int)n, da + 16 * n, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(out, da + 16 * n, n * 32, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+}  // extern "C"

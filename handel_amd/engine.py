@@ -1,0 +1,174 @@
+"""Host wrapper around one hg_ctx (include/handel_gpu.h).
+
+`Engine` is the batched replacement for the reference's one-at-a-time crypto
+calls: it owns a GPU context, the decoded registry and the
+hashed message, and exposes every C-ABI entry point with numpy/bytes
+arguments. Device-resident variants take raw device pointers (e.g. from
+torch tensors) and a HIP stream handle.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import HandelGPUError
+
+FLAVORS = {"go": _lib.HG_FLAVOR_GO, "bn256/go": _lib.HG_FLAVOR_GO,
+           "cf": _lib.HG_FLAVOR_CF, "bn256/cf": _lib.HG_FLAVOR_CF, "bn256": _lib.HG_FLAVOR_CF}
+
+REQ_DTYPE = np.dtype([("offset", "<u4"), ("bitlen", "<u4"), ("level_size", "<u4"), ("word_offset", "<u4")])
+
+
+def _ptr(a) -> Optional[int]:
+    if a is None:
+        return None
+    if isinstance(a, (bytes, bytearray)):
+        return ctypes.cast(ctypes.c_char_p(bytes(a)), ctypes.c_void_p).value
+    return a.ctypes.data
+
+
+def _u8(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8)
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+class Engine:
+    """One verification context on one GPU (hg_create)."""
+
+    def __init__(self, device: int = 0, flavor: str = "go"):
+        self.L = _lib.load()
+        self.flavor_name = flavor
+        self.flavor = FLAVORS[flavor]
+        h = ctypes.c_void_p()
+        rc = self.L.hg_create(device, self.flavor, ctypes.byref(h))
+        if rc != 0:
+            raise HandelGPUError(f"hg_create failed: code {rc}")
+        self.ctx = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.hg_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str, ok=(0,)):
+        if rc not in ok:
+            err = self.L.hg_last_error(self.ctx)
+            raise HandelGPUError(f"{what}: code {rc}: {err.decode() if err else ''}")
+        return rc
+
+    def code_string(self, code: int) -> str:
+        return self.L.hg_code_string(int(code), self.flavor).decode()
+
+    # ----------------------------------------------------------- setup
+    def set_message(self, msg: bytes) -> int:
+        """hashedMessage once per message; returns HG_OK or HG_ERR_HASH_EOF."""
+        m = _u8(msg)
+        return self._check(self.L.hg_set_message(self.ctx, _ptr(m) if len(m) else None, len(m)),
+                           "hg_set_message", ok=(0, _lib.HG_ERR_HASH_EOF))
+
+    def registry_load(self, pks: bytes) -> np.ndarray:
+        a = _u8(pks)
+        n = len(a) // 128
+        codes = np.zeros(n, dtype=np.int32)
+        rc = self.L.hg_registry_load(self.ctx, _ptr(a), n, _ptr(codes))
+        self._check(rc, "hg_registry_load", ok=(0, _lib.HG_ERR_PK_UNMARSHAL))
+        return codes
+
+    # ----------------------------------------------------------- batch verification
+    def verify_batch(self, pks: bytes, sigs: bytes) -> np.ndarray:
+        a, b = _u8(pks), _u8(sigs)
+        n = len(b) // 64
+        if len(a) != 128 * n:
+            raise ValueError("pks must hold 128 bytes per signature")
+        codes = np.zeros(n, dtype=np.int32)
+        self._check(self.L.hg_verify_batch(self.ctx, _ptr(a), _ptr(b), n, _ptr(codes)), "hg_verify_batch")
+        return codes
+
+    def verify_batch_device(self, d_pks: int, d_sigs: int, n: int, d_codes: int, stream: int = 0):
+        self._check(self.L.hg_verify_batch_device(self.ctx, d_pks, d_sigs, n, d_codes, stream or None),
+                    "hg_verify_batch_device")
+
+    def verify_aggregate(self, reqs: np.ndarray, words: np.ndarray, sigs: bytes, want_agg: bool = False):
+        reqs = np.ascontiguousarray(reqs, dtype=REQ_DTYPE)
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        s = _u8(sigs)
+        n = len(reqs)
+        codes = np.zeros(n, dtype=np.int32)
+        agg = np.zeros(n * 128, dtype=np.uint8) if want_agg else None
+        self._check(self.L.hg_verify_aggregate(self.ctx, _ptr(reqs), n, _ptr(words) if len(words) else None,
+                                               len(words), _ptr(s), _ptr(codes), _ptr(agg)),
+                    "hg_verify_aggregate")
+        return (codes, agg.tobytes()) if want_agg else codes
+
+    def verify_aggregate_device(self, d_reqs: int, n: int, d_words: int, d_sigs: int, d_codes: int,
+                                d_agg: int = 0, stream: int = 0):
+        self._check(self.L.hg_verify_aggregate_device(self.ctx, d_reqs, n, d_words, d_sigs, d_codes,
+                                                      d_agg or None, stream or None),
+                    "hg_verify_aggregate_device")
+
+    def aggregate_pk(self, reqs: np.ndarray, words: np.ndarray) -> Tuple[bytes, np.ndarray]:
+        reqs = np.ascontiguousarray(reqs, dtype=REQ_DTYPE)
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        n = len(reqs)
+        codes = np.zeros(n, dtype=np.int32)
+        out = np.zeros(n * 128, dtype=np.uint8)
+        self._check(self.L.hg_aggregate_pk(self.ctx, _ptr(reqs), n, _ptr(words) if len(words) else None,
+                                           len(words), _ptr(out), _ptr(codes)), "hg_aggregate_pk")
+        return out.tobytes(), codes
+
+    def combine_g1(self, a: bytes, b: bytes) -> Tuple[bytes, np.ndarray]:
+        x, y = _u8(a), _u8(b)
+        n = len(x) // 64
+        out = np.zeros(n * 64, dtype=np.uint8)
+        codes = np.zeros(n, dtype=np.int32)
+        self._check(self.L.hg_combine_g1(self.ctx, _ptr(x), _ptr(y), n, _ptr(out), _ptr(codes)), "hg_combine_g1")
+        return out.tobytes(), codes
+
+    def pair(self, g1s: bytes, g2s: bytes) -> Tuple[bytes, np.ndarray]:
+        x, y = _u8(g1s), _u8(g2s)
+        n = len(x) // 64
+        out = np.zeros(n * 384, dtype=np.uint8)
+        codes = np.zeros(n, dtype=np.int32)
+        self._check(self.L.hg_pair(self.ctx, _ptr(x), _ptr(y), n, _ptr(out), _ptr(codes)), "hg_pair")
+        return out.tobytes(), codes
+
+    def keygen(self, scalars_be: bytes) -> bytes:
+        s = _u8(scalars_be)
+        n = len(s) // 32
+        out = np.zeros(n * 128, dtype=np.uint8)
+        self._check(self.L.hg_keygen(self.ctx, _ptr(s), n, _ptr(out)), "hg_keygen")
+        return out.tobytes()
+
+    def sign(self, scalars_be: bytes) -> bytes:
+        s = _u8(scalars_be)
+        n = len(s) // 32
+        out = np.zeros(n * 64, dtype=np.uint8)
+        self._check(self.L.hg_sign(self.ctx, _ptr(s), n, _ptr(out)), "hg_sign")
+        return out.tobytes()
+
+    def fp_mul(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        b = np.ascontiguousarray(b, dtype=np.uint32)
+        n = a.shape[0]
+        out = np.zeros((n, 8), dtype=np.uint32)
+        self._check(self.L.hg_debug_fp_mul(self.ctx, _ptr(a), _ptr(b), n, _ptr(out)), "hg_debug_fp_mul")
+        return out
+
+    def sync(self):
+        self._check(self.L.hg_sync(self.ctx), "hg_sync")
+
+
+def requests_array(items: Sequence[Tuple[int, int, int, int]]) -> np.ndarray:
+    return np.array(items, dtype=REQ_DTYPE)

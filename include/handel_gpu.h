@@ -1,0 +1,134 @@
+/*
+ * handel_gpu.h — C ABI of the MI355X BN256 BLS verification engine.
+ *
+ * This is the drop-in boundary for Handel's crypto plugin interfaces
+ * (crypto.go:14-54: PublicKey / Signature / Constructor / MultiSignature)
+ * on the bn256 path. A Go maintainer binds it with cgo;
+ * the Python host package handel_amd binds it with ctypes. Plain pointers
+ * and sizes only; every entry point is thread-safe per context (a mutex
+ * serialises submitters, matching the concurrent Handel instances of
+ * simul/node/main.go:63-77).
+ *
+ * Byte formats are the reference's marshals:
+ *   G1 (signature)  64 B  = x || y, 32-byte big-endian affine coords, zeros = infinity
+ *   G2 (public key) 128 B = x.x || x.y || y.x || y.y (x = x.x*i + x.y), zeros = infinity
+ *   GT              384 B = x/crypto GT.Marshal order
+ *   bitsets          willf/bitset words: bit i = word[i >> 6] bit (i & 63)
+ */
+#ifndef HANDEL_GPU_H
+#define HANDEL_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Per-check result codes. Each maps 1:1 to the error the reference returns
+ * (hg_code_string gives the exact text for the chosen flavor). */
+enum hg_code {
+  HG_OK = 0,                /* nil */
+  HG_ERR_SIG_INVALID = 1,   /* "bn256: signature invalid"            bn256/go/bn256.go:91 */
+  HG_ERR_HASH_EOF = 2,      /* "EOF" (hashedMessage, digest >= n)     bn256/go/bn256.go:210-218 */
+  HG_ERR_LEVEL = 3,         /* "handel: inconsistent bitset with given level" processing.go:350-352 */
+  HG_ERR_PK_UNMARSHAL = 4,  /* "unable to unmarshal"                  bn256/go/bn256.go:117 */
+  HG_ERR_SIG_UNMARSHAL = 5, /* "bn256: multisig can't unmarshal"      bn256/go/bn256.go:186 */
+  HG_ERR_EMPTY_AGG = 6,     /* empty bitset: the reference dereferences a nil *G2 (panic) */
+  HG_ERR_CF_EXCEEDS = 7,    /* cloudflare: "bn256: coordinate exceeds modulus" */
+  HG_ERR_CF_MALFORMED = 8,  /* cloudflare: "bn256: malformed point" */
+  HG_ERR_CF_SHORT = 9,      /* cloudflare: "bn256: not enough data" */
+  HG_ERR_ARG = 100,         /* bad argument to this API */
+  HG_ERR_DEVICE = 101       /* HIP runtime failure (see hg_last_error) */
+};
+
+/* Which upstream library's Unmarshal rules to mirror (simul/lib/config.go:211-225). */
+enum hg_flavor {
+  HG_FLAVOR_GO = 0, /* golang.org/x/crypto/bn256  ("bn256/go") */
+  HG_FLAVOR_CF = 1  /* github.com/cloudflare/bn256 ("bn256", "bn256/cf") */
+};
+
+typedef struct hg_ctx hg_ctx;
+
+/* One aggregate-verification request (processing.go:342-368 verifySignature):
+ * the level's registry range starts at `offset` (partitioner.go rangeLevel min),
+ * `level_size` = max - min, the bitset has `bitlen` bits stored at
+ * words[word_offset ...]. bitlen != level_size -> HG_ERR_LEVEL. */
+typedef struct {
+  uint32_t offset;
+  uint32_t bitlen;
+  uint32_t level_size;
+  uint32_t word_offset;
+} hg_request;
+
+/* Context: owns a device, the decoded registry, the hashed message and the
+ * precomputed G2Base line table. Replaces bn256.NewConstructor() + the
+ * package-level G2Base (bn256/go/bn256.go:22,28-52). */
+int hg_create(int device, int flavor, hg_ctx** out);
+void hg_destroy(hg_ctx* ctx);
+const char* hg_last_error(hg_ctx* ctx);
+const char* hg_code_string(int code, int flavor);
+int hg_version(void);
+
+/* Registry.Identities(...).PublicKey() source: uploads n marshalled G2
+ * public keys (PublicKey.UnmarshalBinary, bn256/go/bn256.go:113-120), decoding
+ * them on the GPU. codes (nullable, n entries) receives per-key decode codes;
+ * returns HG_OK only if every key decoded. */
+int hg_registry_load(hg_ctx* ctx, const uint8_t* pks, size_t n, int32_t* codes);
+size_t hg_registry_size(hg_ctx* ctx);
+
+/* hashedMessage (bn256/go/bn256.go:210-218) computed once per message and
+ * cached on the device. Returns HG_OK or HG_ERR_HASH_EOF. */
+int hg_set_message(hg_ctx* ctx, const uint8_t* msg, size_t len);
+
+/* n independent PublicKey.VerifySignature(msg, sig) checks (bn256/go:82-94;
+ * simul/p2p/aggregator.go:244). pks: n*128 B, sigs: n*64 B, codes: n. */
+int hg_verify_batch(hg_ctx* ctx, const uint8_t* pks, const uint8_t* sigs, size_t n, int32_t* codes);
+
+/* Same, with pks/sigs/codes already resident in device memory; `stream` is a
+ * hipStream_t (NULL = the context's stream). Asynchronous on the stream. */
+int hg_verify_batch_device(hg_ctx* ctx, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n, int32_t* d_codes,
+                           void* stream);
+
+/* n aggregate checks against the registry: the Combine fold over the set
+ * bits of each request's level range, then VerifySignature
+ * (processing.go:342-368; crypto.go:120-137 for a full-registry request).
+ * agg_pk_out (nullable): n*128 B marshal of each aggregate public key. */
+int hg_verify_aggregate(hg_ctx* ctx, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
+                        const uint8_t* sigs, int32_t* codes, uint8_t* agg_pk_out);
+
+/* Device-resident variant (reqs, words, sigs, codes, agg out on the device). */
+int hg_verify_aggregate_device(hg_ctx* ctx, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                               const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg_pk_out, void* stream);
+
+/* Batched PublicKey.Combine fold only: n requests -> n*128 B aggregate keys
+ * (bn256/go/bn256.go:97-105). codes: HG_OK, HG_ERR_LEVEL or HG_ERR_EMPTY_AGG. */
+int hg_aggregate_pk(hg_ctx* ctx, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
+                    uint8_t* agg_pk_out, int32_t* codes);
+
+/* Batched SigBLS.Combine (bn256/go/bn256.go:192-200): out[i] = a[i] + b[i]. */
+int hg_combine_g1(hg_ctx* ctx, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out, int32_t* codes);
+
+/* bn256.Pair(g1[i], g2[i]).Marshal() — the GT values the reference compares
+ * in VerifySignature (bn256/go/bn256.go:88-89); parity probe. */
+int hg_pair(hg_ctx* ctx, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t* gt_out, int32_t* codes);
+
+/* Batch keygen / signing for fixtures and simulation start-up:
+ * NewKeyPair's pk = k * G2 (bn256/go/bn256.go:129-142) and Sign's
+ * sig = k * H(msg) (bn256/go/bn256.go:146-154) for n big-endian 32-byte
+ * scalars. hg_sign needs hg_set_message first (returns HG_ERR_HASH_EOF when
+ * the message cannot be hashed). */
+int hg_keygen(hg_ctx* ctx, const uint8_t* scalars_be, size_t n, uint8_t* pks_out);
+int hg_sign(hg_ctx* ctx, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out);
+
+/* Self test of the field multiplier: out = a*b mod p on plain 256-bit
+ * little-endian 32-bit words (8 per element). */
+int hg_debug_fp_mul(hg_ctx* ctx, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out);
+
+/* Wait for all work submitted on the context's stream. */
+int hg_sync(hg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HANDEL_GPU_H */

@@ -1,0 +1,151 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Integer/byte work, so the bar is bit-exact: field products, GT marshals
+(bn256.Pair(...).Marshal(), bn256/go/bn256.go:88-89), verdict codes, and
+marshalled aggregate keys / combined signatures.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import bn256_oracle as O
+from oracle import ref_lib as R
+from tests import _fixtures as F
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fp_mul_matches_bigint(engine):
+    rng = np.random.default_rng(1)
+    n = 257
+    vals = [0, 1, 2, O.P - 1, O.P - 2, (1 << 255), O.P // 2]
+    a_int = vals + [int.from_bytes(rng.bytes(32), "little") % O.P for _ in range(n - len(vals))]
+    b_int = list(reversed(vals)) + [int.from_bytes(rng.bytes(32), "little") % O.P for _ in range(n - len(vals))]
+
+    def words(xs):
+        return np.array([[(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)] for x in xs], dtype=np.uint32)
+
+    out = engine.fp_mul(words(a_int), words(b_int))
+    got = [sum(int(w) << (32 * i) for i, w in enumerate(row)) for row in out]
+    want = [(x * y) % O.P for x, y in zip(a_int, b_int)]
+    assert got == want
+
+
+def test_pair_matches_oracle_gt_bytes(engine):
+    cases = [(O.G1_GEN, O.G2_GEN), (O.g1_mul(O.G1_GEN, 7), O.G2_GEN), (O.G1_GEN, O.g2_mul(O.G2_GEN, 11)),
+             (O.g1_mul(O.G1_GEN, 123456789), O.g2_mul(O.G2_GEN, 987654321)), (None, O.G2_GEN), (O.G1_GEN, None)]
+    g1 = b"".join(O.g1_marshal(p) for p, _ in cases)
+    g2 = b"".join(O.g2_marshal(q) for _, q in cases)
+    gt, codes = engine.pair(g1, g2)
+    assert list(codes) == [0] * len(cases)
+    for i, (p, q) in enumerate(cases):
+        want = O.f12_marshal(O.pair(p, q))
+        assert gt[384 * i:384 * (i + 1)] == want, f"pair case {i}"
+
+
+def test_keygen_and_sign_match_oracle(engine):
+    ks = F.scalars(40, b"keygen")
+    kb = F.scalar_bytes(ks)
+    assert engine.keygen(kb) == R.g2_scalar_base(kb)
+    assert engine.set_message(F.LIB_MESSAGE) == 0
+    assert engine.sign(kb) == R.sign(F.LIB_MESSAGE, kb)
+
+
+def test_verify_batch_matches_oracle(engine):
+    _, pks, sigs = F.keys_and_sigs(64, seed=b"vb")
+    sigs = F.tamper(sigs, every=8)
+    assert engine.set_message(F.LIB_MESSAGE) == 0
+    got = engine.verify_batch(pks, sigs)
+    want = R.verify_batch(F.LIB_MESSAGE, pks, sigs, nthreads=8)
+    assert list(got) == list(want)
+    assert (got == 1).sum() == 8 and (got == 0).sum() == 56
+
+
+def test_verify_batch_edge_cases(engine):
+    msg = F.TEST_MESSAGES[0]
+    ks, pks, sigs = F.keys_and_sigs(4, msg=msg, seed=b"edge")
+    z128, z64 = bytes(128), bytes(64)
+    off_curve_g1 = (1).to_bytes(32, "big") + (1).to_bytes(32, "big")
+    off_curve_g2 = bytes(127) + b"\x01"
+    cases_pk = [pks[0:128], z128, z128, pks[128:256], off_curve_g2, pks[384:512]]
+    cases_sig = [sigs[0:64], z64, sigs[64:128], z64, sigs[192:256], off_curve_g1]
+    pk_b, sig_b = b"".join(cases_pk), b"".join(cases_sig)
+    assert engine.set_message(msg) == 0
+    got = list(engine.verify_batch(pk_b, sig_b))
+    # oracle verdicts
+    want = []
+    for p, s in zip(cases_pk, cases_sig):
+        P, e1 = O.g2_unmarshal(p, "go")
+        S, e2 = O.g1_unmarshal(s, "go")
+        if e1:
+            want.append(R.RC_PK_UNMARSHAL)
+        elif e2:
+            want.append(R.RC_SIG_UNMARSHAL)
+        else:
+            want.append(0 if O.verify_signature(P, msg, S) is None else 1)
+    assert got == want
+    assert got[1] == 0  # infinity pk with infinity sig verifies (e(H,inf) = 1 = e(inf,G2))
+
+
+def test_hash_reject_message(engine):
+    _, pks, sigs = F.keys_and_sigs(2, msg=F.TEST_MESSAGES[1], seed=b"rej")
+    assert engine.set_message(F.REJECT_MESSAGES[0]) == 2
+    assert list(engine.verify_batch(pks, sigs)) == [2, 2]
+
+
+def test_combine_g1_matches_oracle(engine):
+    _, _, sigs = F.keys_and_sigs(9, seed=b"comb")
+    a = sigs[:4 * 64] + sigs[0:64] + bytes(64)
+    b = sigs[4 * 64:8 * 64] + O.g1_marshal(O.g1_neg(O.g1_unmarshal(sigs[0:64])[0])) + sigs[64:128]
+    out, codes = engine.combine_g1(a, b)
+    assert list(codes) == [0] * 6
+    for i in range(6):
+        assert out[64 * i:64 * i + 64] == R.g1_add(a[64 * i:64 * i + 64], b[64 * i:64 * i + 64])
+    assert out[4 * 64:5 * 64] == bytes(64)  # sig + (-sig) = infinity
+
+
+def test_verify_aggregate_matches_oracle(engine):
+    n_reg = 50
+    ks, reg, _ = F.keys_and_sigs(n_reg, seed=b"agg")
+    msg = F.LIB_MESSAGE
+    assert list(engine.registry_load(reg)) == [0] * n_reg
+    assert engine.set_message(msg) == 0
+    rng = np.random.default_rng(7)
+    # level ranges of a 50-node Handel registry seen from node 3 (partitioner rangeLevel)
+    ranges = []
+    for lvl in range(1, O.log2_ceil(n_reg) + 1):
+        rl, err = O.range_level(3, n_reg, lvl)
+        if err is None:
+            ranges.append((rl[0], rl[1] - rl[0]))
+    ranges.append((0, n_reg))  # full registry (VerifyMultiSignature)
+    bitsets = F.random_bitsets(rng, [s for _, s in ranges])
+    bitsets[0] = [True] * ranges[0][1]
+    sigs = b""
+    for (off, size), bits in zip(ranges, bitsets):
+        agg = None
+        for i, b in enumerate(bits):
+            if b:
+                s = O.g1_mul(O.hashed_message(msg)[0], ks[off + i])
+                agg = s if agg is None else O.g1_add(agg, s)
+        sigs += O.g1_marshal(agg)
+    sigs = bytearray(sigs)
+    sigs[64:128] = F.tamper(bytes(sigs[64:128]), every=1)  # one bad aggregate
+    reqs, words = F.pack_requests(ranges, bitsets)
+    reqs.append((0, 3, 4, 0))  # bitlen != level size
+    bitsets.append([True] * 3)
+    sigs += bytes(sigs[0:64])
+    codes, agg = engine.verify_aggregate(np.array(reqs, dtype=engine_req_dtype()), words, bytes(sigs), want_agg=True)
+    woff = np.array([r[3] for r in reqs], dtype=np.uint64)
+    want, want_agg = R.verify_aggregate(msg, reg, [r[0] for r in reqs], [r[1] for r in reqs],
+                                        [r[2] for r in reqs], words, woff, bytes(sigs), nthreads=4,
+                                        want_agg=True)
+    assert list(codes) == list(want)
+    for i in range(len(reqs)):
+        if want[i] in (0, 1):
+            assert agg[128 * i:128 * (i + 1)] == want_agg[128 * i:128 * (i + 1)], f"agg {i}"
+    assert codes[1] == 1 and codes[-1] == 3 and codes[0] == 0
+
+
+def engine_req_dtype():
+    from handel_amd.engine import REQ_DTYPE
+    return REQ_DTYPE
