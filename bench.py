@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Headline benchmark: BN256 BLS verifications/s at batch 4096 on MI355X.
+
+Workload (BASELINE.json configs[1]): one step =
+4096 independent PublicKey.VerifySignature(lib.Message, sig) checks
+(bn256/go/bn256.go:82-94) with 1/8 of the signatures tampered, inputs
+(marshalled pks and sigs) already resident in HBM, verdict codes written
+back to HBM, then the verdict bitset gathered to rank 0 over RCCL.
+Keys/signatures are synthetic (seeded scalars, keygen/sign on the GPU).
+
+Multi-GPU: one process per GPU (torchrun), every rank verifies its own batch
+of 4096 (weak scaling, no data-path collective); the only exchange is the
+all_gather of 512-byte verdict bitsets.
+
+Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from handel_amd.engine import Engine  # noqa: E402
+
+LIB_MESSAGE = b"Everything that is beautiful and noble is the product of reason and calculation."
+ORDER = 65000549695646603732796438742359905742570406053903786389881062969044166799969
+P = 65000549695646603732796438742359905742825358107623003571877145026864184071783
+G1_GEN_BYTES = (1).to_bytes(32, "big") + (P - 2).to_bytes(32, "big")
+
+# Algorithmic work per check, fixed before tuning by the oracle's op counter
+# (oracle/bn256_ref.c, fast=2: one multi-Miller loop over 6u+2 with the pk
+# lines on the fly and the G2Base lines from a table, one final
+# exponentiation, Karatsuba tower formulas): Fp multiplications per check.
+# tests/test_oracle.py pins this number.
+FPMUL_PER_CHECK = 25271
+# u32 x u32 multiply-adds per Fp multiplication (8-limb CIOS: 2*8^2 + 8)
+MADS_PER_FPMUL = 136
+# Peak v_mad_u64_u32 rate, measured by tools/intrate.hip on MI355X
+# (profiles/r01_intrate.jsonl; half the VALU rate: 256 CU x 4 SIMD x 32 lanes
+# x 2.4 GHz / 2 = 39.3 T/s spec-derived).
+P_MAD_TOPS = 33.19
+
+
+def seeded_scalars(n: int, seed: int) -> bytes:
+    """n secret keys in [1, n) from a seeded generator (RandomG2 rejection rule)."""
+    rng = np.random.default_rng(seed)
+    out = bytearray()
+    while len(out) < 32 * n:
+        k = int.from_bytes(rng.bytes(32), "big")
+        if 0 < k < ORDER:
+            out += k.to_bytes(32, "big")
+    return bytes(out)
+
+
+def make_batch(eng: Engine, n: int, seed: int):
+    kb = seeded_scalars(n, seed)
+    pks = eng.keygen(kb)
+    sigs = bytearray(eng.sign(kb))
+    # tamper 1/8 of the signatures: sig + G1
+    idx = list(range(0, n, 8))
+    a = b"".join(bytes(sigs[64 * i:64 * i + 64]) for i in idx)
+    bad, codes = eng.combine_g1(a, G1_GEN_BYTES * len(idx))
+    assert not codes.any()
+    for j, i in enumerate(idx):
+        sigs[64 * i:64 * i + 64] = bad[64 * j:64 * j + 64]
+    expect = np.zeros(n, dtype=np.int32)
+    expect[idx] = 1
+    return pks, bytes(sigs), expect
+
+
+def cpu_baseline(n_sample: int, pks: bytes, sigs: bytes, expect: np.ndarray):
+    """The reference algorithm restated in C (oracle/bn256_ref.c, 'port'):
+    two full pairings + GT compare per check, timed on this host's cores."""
+    from oracle import ref_lib as R
+
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    codes = R.verify_batch(LIB_MESSAGE, pks[:128 * n_sample], sigs[:64 * n_sample], nthreads=threads, fast=0)
+    dt = time.perf_counter() - t0
+    assert np.array_equal(codes, expect[:n_sample]), "CPU oracle verdicts differ"
+    return {"value": round(n_sample / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
+            "sample": f"{n_sample} checks of the same batch (lib.Message, 1/8 tampered), reference algorithm "
+                      f"(2 pairings + GT compare), {threads} threads, {dt:.2f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    eng = Engine(device=local, flavor="go")
+    assert eng.set_message(LIB_MESSAGE) == 0
+    n = args.batch
+    pks, sigs, expect = make_batch(eng, n, seed=1234 + rank)
+    d_pks = torch.frombuffer(bytearray(pks), dtype=torch.uint8).to(dev)
+    d_sigs = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
+    d_codes = torch.zeros(n, dtype=torch.int32, device=dev)
+    nbits = (n + 7) // 8 * 8
+    weights = (2 ** torch.arange(8, device=dev, dtype=torch.int32)).view(1, 8)
+    gathered = [torch.zeros(nbits // 8, dtype=torch.uint8, device=dev) for _ in range(world)]
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.verify_batch_device(d_pks.data_ptr(), d_sigs.data_ptr(), n, d_codes.data_ptr(), stream.cuda_stream)
+        ok = torch.zeros(nbits, dtype=torch.int32, device=dev)
+        ok[:n] = (d_codes == 0).to(torch.int32)
+        bits = (ok.view(-1, 8) * weights).sum(dim=1).to(torch.uint8)  # verdict bitset (bit i = check i valid)
+        if dist:
+            tdist.all_gather(gathered, bits)
+        else:
+            gathered[0].copy_(bits)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    got = d_codes.cpu().numpy()
+    assert np.array_equal(got, expect), f"GPU verdicts differ from the expected pattern: {np.flatnonzero(got != expect)[:8]}"
+
+    eng.timing_enable(True)
+    eng.timing_read()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    dt = time.perf_counter() - t0
+    kern_ms, launches = eng.timing_read()
+    eng.timing_enable(False)
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    got = d_codes.cpu().numpy()
+    assert np.array_equal(got, expect)
+
+    total = n * args.steps * world
+    value = total / dt
+    avg_kernel_ms = kern_ms / max(launches, 1)
+    achieved = n * FPMUL_PER_CHECK * MADS_PER_FPMUL / (avg_kernel_ms * 1e-3) / 1e12
+    roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": P_MAD_TOPS, "unit": "Tmad/s",
+                "frac": round(achieved / P_MAD_TOPS, 4), "traffic": None,
+                "kernel": "k_verify", "kernel_ms": round(avg_kernel_ms, 4),
+                "work_per_check": f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            cpu = cpu_baseline(min(n, 4096), pks, sigs, expect)
+        except Exception as e:  # pragma: no cover - reported, not fatal
+            cpu = {"error": str(e)}
+    if rank == 0:
+        line = {
+            "metric": "BN254 aggregate-sig verifications/sec (batch 4096)",
+            "value": round(value, 1),
+            "unit": "verifications/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (26-bit-limb Fp, 64-bit accumulators)",
+            "data": "synthetic (seeded keys, lib.Message, 1/8 tampered signatures)",
+            "config": {"workload": "config 2: 4096 independent BLS pairing checks per GPU (bn256, dclxvi curve)",
+                       "batch_per_gpu": n, "message": "lib.Message (81 B)", "parallelism": f"dp{world} (replicated registry, sharded batches)"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    eng.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

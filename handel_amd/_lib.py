@@ -55,6 +55,8 @@ SIGNATURES = {
     "hg_keygen": (_I, [_P, _P, _SZ, _P]),
     "hg_sign": (_I, [_P, _P, _SZ, _P]),
     "hg_debug_fp_mul": (_I, [_P, _P, _P, _SZ, _P]),
+    "hg_timing_enable": (_I, [_P, _I]),
+    "hg_timing_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
     "hg_sync": (_I, [_P]),
 }
 

@@ -164,7 +164,22 @@ struct hg_ctx {
   DevBuf<int32_t> codes_a, codes_b, codes_c;
   DevBuf<hg_request> reqs;
   DevBuf<uint64_t> words;
+  // optional per-launch timing of the pairing-check kernel (bench roofline)
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> verify_events;
 };
+
+static void timed_verify(hg_ctx* c, const CheckIn* in, int n, int32_t* codes, hipStream_t s) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->timing && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) {
+    (void)hipEventRecord(a, s);
+    launch_verify(in, n, c->d_lines, c->d_h, codes, s);
+    (void)hipEventRecord(b, s);
+    c->verify_events.emplace_back(a, b);
+    return;
+  }
+  launch_verify(in, n, c->d_lines, c->d_h, codes, s);
+}
 
 #define HG_CHECK(ctx, expr)                                                        \
   do {                                                                             \
@@ -329,7 +344,7 @@ static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uin
     return check_launch(c);
   }
   launch_checks_from_points(c->pts2.p, c->pts1.p, (int)n, c->checks.p, s);
-  launch_verify(c->checks.p, (int)n, c->d_lines, c->d_h, d_codes, s);
+  timed_verify(c, c->checks.p, (int)n, d_codes, s);
   return check_launch(c);
 }
 
@@ -392,7 +407,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   k_agg_codes<<<nb(n), 256, 0, s>>>(c->codes_b.p, d_lvl, c->hash_eof ? 1 : 0, (int)n, d_codes);
   if (!c->hash_eof) {
     launch_sig_into_checks(c->pts1.p, (int)n, c->checks.p, s);
-    launch_verify(c->checks.p, (int)n, c->d_lines, c->d_h, d_codes, s);
+    timed_verify(c, c->checks.p, (int)n, d_codes, s);
   }
   return check_launch(c);
 }
@@ -565,6 +580,34 @@ int hg_sign(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out) {
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(sigs_out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_timing_enable(hg_ctx* c, int on) {
+  if (!c) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->timing = on != 0;
+  return HG_OK;
+}
+
+int hg_timing_read(hg_ctx* c, double* total_ms, int* launches) {
+  if (!c || !total_ms || !launches) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  double tot = 0;
+  int k = 0;
+  for (auto& pr : c->verify_events) {
+    float ms = 0;
+    HG_CHECK(c, hipEventSynchronize(pr.second));
+    HG_CHECK(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+    tot += ms;
+    k++;
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  c->verify_events.clear();
+  *total_ms = tot;
+  *launches = k;
   return HG_OK;
 }
 

@@ -166,6 +166,15 @@ class Engine:
         self._check(self.L.hg_debug_fp_mul(self.ctx, _ptr(a), _ptr(b), n, _ptr(out)), "hg_debug_fp_mul")
         return out
 
+    def timing_enable(self, on: bool = True):
+        self._check(self.L.hg_timing_enable(self.ctx, int(on)), "hg_timing_enable")
+
+    def timing_read(self) -> Tuple[float, int]:
+        ms = ctypes.c_double()
+        k = ctypes.c_int()
+        self._check(self.L.hg_timing_read(self.ctx, ctypes.byref(ms), ctypes.byref(k)), "hg_timing_read")
+        return ms.value, k.value
+
     def sync(self):
         self._check(self.L.hg_sync(self.ctx), "hg_sync")
 

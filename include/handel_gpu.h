@@ -125,6 +125,12 @@ int hg_sign(hg_ctx* ctx, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out)
  * little-endian 32-bit words (8 per element). */
 int hg_debug_fp_mul(hg_ctx* ctx, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out);
 
+/* Measurement hooks: when enabled, every launch of the pairing-check kernel
+ * is bracketed by HIP events on the stream it runs on; hg_timing_read
+ * returns (and clears) the summed kernel time and the number of launches. */
+int hg_timing_enable(hg_ctx* ctx, int on);
+int hg_timing_read(hg_ctx* ctx, double* total_ms, int* launches);
+
 /* Wait for all work submitted on the context's stream. */
 int hg_sync(hg_ctx* ctx);
 

@@ -87,8 +87,20 @@ static inline void fp_neg(fp* r, const fp* a) {
   fp z = {{0, 0, 0, 0}};
   fp_sub(r, &z, a);
 }
+/* Op counter: Fp multiplications (squarings included) on this thread. Used
+ * to fix the algorithmic work per check for the roofline (SURVEY.md §8 d). */
+/* Counting is off by default (baseline timing) and meant for one thread. */
+static volatile int g_count_on;
+static uint64_t g_fpmul_count;
+uint64_t ref_fp_mul_count(void) { return g_fpmul_count; }
+void ref_reset_count(int on) {
+  g_fpmul_count = 0;
+  g_count_on = on;
+}
+
 /* CIOS Montgomery multiplication, R = 2^256 */
 static inline void fp_mul(fp* r, const fp* a, const fp* b) {
+  if (g_count_on) g_fpmul_count++;
   uint64_t t[6] = {0, 0, 0, 0, 0, 0};
   for (int i = 0; i < 4; i++) {
     u128 c = 0;
@@ -372,13 +384,43 @@ static void f12_pow_u(fp12* r, const fp12* a) {
   }
   *r = acc;
 }
+/* f *= c + b w + a w^3. Tower view: L0 = (c, 0, 0), L1 = (b, a, 0); the
+ * sparse Karatsuba product costs 13 Fp2 multiplications (39 Fp). */
+static void f6_mul_by_01(fp6* r, const fp6* a, const fp2* b0, const fp2* b1) {
+  fp2 v0, v1, t, s;
+  f2_mul(&v0, &a->c[0], b0);
+  f2_mul(&v1, &a->c[1], b1);
+  fp6 o;
+  f2_add(&t, &a->c[1], &a->c[2]);
+  f2_mul(&t, &t, b1);
+  f2_sub(&t, &t, &v1);
+  f2_mul_xi(&t, &t);
+  f2_add(&o.c[0], &t, &v0);
+  f2_add(&t, &a->c[0], &a->c[1]);
+  f2_add(&s, b0, b1);
+  f2_mul(&t, &t, &s);
+  f2_sub(&t, &t, &v0);
+  f2_sub(&o.c[1], &t, &v1);
+  f2_add(&t, &a->c[0], &a->c[2]);
+  f2_mul(&t, &t, b0);
+  f2_sub(&t, &t, &v0);
+  f2_add(&o.c[2], &t, &v1);
+  *r = o;
+}
 static void f12_mul_line(fp12* f, const fp2* a, const fp2* b, const fp2* c) {
-  fp12 l;
-  for (int k = 0; k < 6; k++) l.c[k] = F2_ZERO;
-  l.c[0] = *c;
-  l.c[1] = *b;
-  l.c[3] = *a;
-  f12_mul(f, f, &l);
+  fp6 A, B, t0, t1, S;
+  split12(f, &A, &B);
+  for (int i = 0; i < 3; i++) f2_mul(&t0.c[i], &A.c[i], c); /* A * L0 */
+  f6_mul_by_01(&t1, &B, b, a);                                 /* B * L1 */
+  f6_add(&S, &A, &B);
+  fp2 cb;
+  f2_add(&cb, c, b);
+  f6_mul_by_01(&S, &S, &cb, a);                                /* (A+B)(L0+L1) */
+  f6_sub(&S, &S, &t0);
+  f6_sub(&S, &S, &t1);
+  f6_mul_tau(&t1, &t1);
+  f6_add(&t0, &t0, &t1);
+  join12(f, &t0, &S);
 }
 
 /* ------------------------------------------------------------------ Miller loop (optate.go) */
@@ -503,6 +545,94 @@ static void miller(fp12* f, const fp2* qx2, const fp2* qy2, const fp* px, const 
   f2_sqr(&r2, qy2);
   line_add(&a, &b, &c, &r, &q2x, qy2, px, py, &r2);
   f12_mul_line(f, &a, &b, &c);
+}
+
+/* G2Base line table: the same line sequence as miller(G2Base, P) with the
+ * G1-dependent factors left out (b = bx * Px, c = cy * Py). */
+#define NLINES 85
+static fp2 G2L_A[NLINES], G2L_BX[NLINES], G2L_CY[NLINES];
+static void build_g2_lines(void) {
+  g2p r;
+  fp2 r2, mqy;
+  fp one = ONE_M;
+  r.x = G2X; r.y = G2Y; r.z = F2_ONE; r.t = F2_ONE;
+  f2_sqr(&r2, &G2Y);
+  f2_neg(&mqy, &G2Y);
+  int s = 0;
+  for (int i = 65; i > 0; i--) {
+    line_double(&G2L_A[s], &G2L_BX[s], &G2L_CY[s], &r, &one, &one);
+    s++;
+    int d = NAF[i - 1];
+    if (d == 0) continue;
+    line_add(&G2L_A[s], &G2L_BX[s], &G2L_CY[s], &r, &G2X, d > 0 ? &G2Y : &mqy, &one, &one, &r2);
+    s++;
+  }
+  fp2 q1x, q1y, q2x;
+  f2_conj(&q1x, &G2X);
+  f2_mul(&q1x, &q1x, &XI_P13);
+  f2_conj(&q1y, &G2Y);
+  f2_mul(&q1y, &q1y, &XI_P12);
+  f2_sqr(&r2, &q1y);
+  line_add(&G2L_A[s], &G2L_BX[s], &G2L_CY[s], &r, &q1x, &q1y, &one, &one, &r2);
+  s++;
+  f2_muls(&q2x, &G2X, &XI_PSQ13);
+  f2_sqr(&r2, &G2Y);
+  line_add(&G2L_A[s], &G2L_BX[s], &G2L_CY[s], &r, &q2x, &G2Y, &one, &one, &r2);
+}
+static inline void fixed_line(fp12* f, int s, const fp* sx, const fp* nsy) {
+  fp2 b, c;
+  f2_muls(&b, &G2L_BX[s], sx);
+  f2_muls(&c, &G2L_CY[s], nsy);
+  f12_mul_line(f, &G2L_A[s], &b, &c);
+}
+/* Multi-Miller loop of the verification product e(P, Q) * e(-S, G2Base):
+ * shared squarings, on-the-fly lines for Q, table lines for G2Base. */
+static void miller2(fp12* f, int use_q, const fp2* qx2, const fp2* qy2, const fp* px, const fp* py, int use_s,
+                    const fp* sx, const fp* sy) {
+  g2p r;
+  fp2 a, b, c, r2, mqy;
+  fp nsy;
+  fp_neg(&nsy, sy);
+  r.x = *qx2; r.y = *qy2; r.z = F2_ONE; r.t = F2_ONE;
+  f2_sqr(&r2, qy2);
+  f2_neg(&mqy, qy2);
+  f12_one(f);
+  int s = 0;
+  for (int i = 65; i > 0; i--) {
+    if (i != 65) f12_sqr(f, f);
+    if (use_q) {
+      line_double(&a, &b, &c, &r, px, py);
+      f12_mul_line(f, &a, &b, &c);
+    }
+    if (use_s) fixed_line(f, s, sx, &nsy);
+    s++;
+    int d = NAF[i - 1];
+    if (d == 0) continue;
+    if (use_q) {
+      line_add(&a, &b, &c, &r, qx2, d > 0 ? qy2 : &mqy, px, py, &r2);
+      f12_mul_line(f, &a, &b, &c);
+    }
+    if (use_s) fixed_line(f, s, sx, &nsy);
+    s++;
+  }
+  if (use_q) {
+    fp2 q1x, q1y, q2x;
+    f2_conj(&q1x, qx2);
+    f2_mul(&q1x, &q1x, &XI_P13);
+    f2_conj(&q1y, qy2);
+    f2_mul(&q1y, &q1y, &XI_P12);
+    f2_sqr(&r2, &q1y);
+    line_add(&a, &b, &c, &r, &q1x, &q1y, px, py, &r2);
+    f12_mul_line(f, &a, &b, &c);
+    f2_muls(&q2x, qx2, &XI_PSQ13);
+    f2_sqr(&r2, qy2);
+    line_add(&a, &b, &c, &r, &q2x, qy2, px, py, &r2);
+    f12_mul_line(f, &a, &b, &c);
+  }
+  if (use_s) {
+    fixed_line(f, s, sx, &nsy);
+    fixed_line(f, s + 1, sx, &nsy);
+  }
 }
 
 static void final_exp(fp12* out, const fp12* in) {
@@ -880,6 +1010,7 @@ void ref_init(void) {
   XI_P13 = GAMMA1[2];  /* xi^((p-1)/3) */
   XI_P12 = GAMMA1[3];  /* xi^((p-1)/2) */
   XI_PSQ13 = GAMMA2[2]; /* xi^((p^2-1)/3) */
+  build_g2_lines();
   g_inited = 1;
 }
 
@@ -1001,6 +1132,12 @@ static void hash_point(g1p* h, const uint8_t k_be[32]) {
   be_to_limbs(k, k_be);
   g1p g = {G1X, G1Y, ONE_M};
   g1_mul(h, &g, k);
+  /* normalise once per message: verify_points reads affine x, y (z = 1) */
+  fp x, y;
+  g1_affine(&x, &y, h);
+  h->x = x;
+  h->y = y;
+  h->z = ONE_M;
 }
 
 /* bn256.Pair(g1, g2).Marshal() for marshalled inputs (flavor go) */
@@ -1025,9 +1162,14 @@ int ref_pair(const uint8_t g1[64], const uint8_t g2[128], uint8_t out[384]) {
 /* Reference VerifySignature on decoded points (two pairings, GT compare) */
 static int verify_points(const g1p* hm, int pk_inf, const fp2* qx, const fp2* qy, int sig_inf,
                          const fp* sx, const fp* sy, int fast) {
-  fp hx, hy;
-  g1_affine(&hx, &hy, hm);
+  fp hx = hm->x, hy = hm->y; /* affine (hash_point normalises) */
   fp12 f1, f2_, e1, e2;
+  if (fast == 2) {
+    /* the algorithm the GPU runs: one multi-Miller loop + one final exp */
+    miller2(&f1, !pk_inf, qx, qy, &hx, &hy, !sig_inf, sx, sy);
+    final_exp(&e1, &f1);
+    return f12_is_one(&e1) ? RC_OK : RC_SIG_INVALID;
+  }
   if (!fast) {
     if (pk_inf) f12_one(&e1);
     else { miller(&f1, qx, qy, &hx, &hy); final_exp(&e1, &f1); }
