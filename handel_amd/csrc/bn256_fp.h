@@ -33,6 +33,9 @@ struct Acc {
   uint64_t c[20];
 };
 
+static constexpr uint32_t kPLimbsC[10] = {HG_PLIMBS};
+__host__ __device__ constexpr uint32_t p_top_limb() { return kPLimbsC[9]; }
+
 HG_DEV uint32_t p_limb(int i) {
   // folded to an immediate after unrolling
   const uint32_t pl[10] = {HG_PLIMBS};

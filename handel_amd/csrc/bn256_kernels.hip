@@ -14,7 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bn256_kernels.h"
-#include "bn256_team.h"
+#include "bn256_g2team.h"
 
 namespace hg {
 
@@ -223,7 +223,7 @@ __global__ void k_g2_lines(LineCoef* tab) {
 // ------------------------------------------------------------------ team Miller loop + final exp
 // LDS layout per team: 12 Fp12 slots followed by the per-check constants.
 enum { S_F = 0, S_A, S_B, S_C, S_D, S_E, S_G, S_H, S_I, S_J, S_K, S_L, kSlots };
-static constexpr int kTeamWords = kSlots * kFp12Words;
+static constexpr int kTeamWords = kSlots * kFp12Words + kG2Regs * 10;
 static constexpr int kTeamsPerBlock = 4;
 
 // the pairing's final exponentiation (x/crypto optate.go finalExponentiation)
@@ -267,88 +267,118 @@ HG_DEV void team_final_exp(const Team& T) {
   t12_mul(T, S_F, S_K, S_J);       // result
 }
 
-// Multiplies f by the line of the moving pairing (pk at H) and by the fixed
-// G2Base line evaluated at the (negated) signature.
+// Per-check inputs of the team Miller loop.
 struct CheckCtx {
-  Fp2 qx, qy, nqy, r2;  // affine pk, -qy, qy^2
-  Fp hx, hy;            // H (affine)
-  Fp sx, nsy;           // -sig = (sx, -sy)
-  bool use_q;           // pk contributes (not infinity)
-  bool use_s;           // sig contributes (not infinity)
+  Fp2 qx, qy;   // affine pk (a dummy valid point when the pk is infinity)
+  Fp hx, hy;    // H (affine)
+  Fp sx, sy;    // sig (affine)
+  bool use_q;   // pk contributes (not infinity)
+  bool use_s;   // sig contributes (not infinity)
 };
 
-HG_DEV void apply_lines(const Team& T, const Fp2& a, const Fp2& bx, const Fp2& cy, const CheckCtx& C,
-                        const LineCoef& L, bool has_fixed) {
-  // branch-free: a point at infinity contributes the line "1" (a = b = 0, c = 1)
-  Fp2 b, c, aa, one, zero;
-  f2_one(one);
-  f2_zero(zero);
-  f2_muls(b, bx, C.hx);
-  f2_muls(c, cy, C.hy);
-  f2_sel(aa, C.use_q, a, zero);
-  f2_sel(b, C.use_q, b, zero);
-  f2_sel(c, C.use_q, c, one);
-  t12_mul_line(T, S_F, S_F, aa, b, c);
-  if (has_fixed) {  // kernel-uniform
-    f2_muls(b, L.bx, C.sx);
-    f2_muls(c, L.cy, C.nsy);
-    f2_sel(aa, C.use_s, L.a, zero);
-    f2_sel(b, C.use_s, b, zero);
-    f2_sel(c, C.use_s, c, one);
-    t12_mul_line(T, S_F, S_F, aa, b, c);
-  }
-}
-
-// f = Miller(pk at H) * Miller(G2Base at -sig); the G2Base lines come from tab.
-HG_DEV void team_miller_check(const Team& T, CheckCtx& C, const LineCoef* tab, bool has_fixed) {
-  const int8_t naf[kNafLen] = HG_NAF;
-  t12_set_one(T, S_F);
-  G2T R;
-  R.x = C.qx;
-  R.y = C.qy;
-  f2_one(R.z);
-  f2_one(R.t);
-  int s = 0;
-  for (int i = kNafLen - 1; i > 0; i--) {
-    Fp2 a, bx, cy;
-    line_double(a, bx, cy, R);
-    if (i != kNafLen - 1) t12_sqr(T, S_F, S_F);
-    apply_lines(T, a, bx, cy, C, tab[s], has_fixed);
-    s++;
-    int d = naf[i - 1];
-    if (d != 0) {
-      line_add(a, bx, cy, R, C.qx, d > 0 ? C.qy : C.nqy, C.r2);
-      apply_lines(T, a, bx, cy, C, tab[s], has_fixed);
-      s++;
-    }
-  }
+// Writes the team's G2 register file: point R = (Q, 1, 1), Q, -Qy, Qy^2, the
+// Frobenius images q1 = pi(Q), -q2 = (Qx gamma2[2], Qy) (optate.go miller),
+// the G1 points and constants.
+HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
   const Fp2 g1[6] = HG_GAMMA1;
   const Fp g2[6] = HG_GAMMA2;
-  Fp2 q1x, q1y, t, r2;
+  Fp2 nqy, r2, q1x, q1y, q1r2, q2x, t, one2, zero2;
+  f2_neg(nqy, C.qy);
+  f2_sqr(r2, C.qy);
   f2_conj(t, C.qx);
   f2_mul(q1x, t, g1[2]);
   f2_conj(t, C.qy);
   f2_mul(q1y, t, g1[3]);
-  f2_sqr(r2, q1y);
-  {
-    Fp2 a, bx, cy;
-    line_add(a, bx, cy, R, q1x, q1y, r2);
-    apply_lines(T, a, bx, cy, C, tab[s], has_fixed);
-    s++;
-  }
-  Fp2 q2x;
+  f2_sqr(q1r2, q1y);
   f2_muls(q2x, C.qx, g2[2]);
-  {
-    Fp2 a, bx, cy;
-    line_add(a, bx, cy, R, q2x, C.qy, C.r2);
-    apply_lines(T, a, bx, cy, C, tab[s], has_fixed);
+  f2_one(one2);
+  f2_zero(zero2);
+  Fp zero, one, nsy;
+  fp_zero(zero);
+  fp_one(one);
+  fp_neg(nsy, C.sy);
+  if (T.tl == 0) {
+    auto put2 = [&](int rx, const Fp2& v) {
+      st_fp(F + rx * 10, v.x);
+      st_fp(F + (rx + 1) * 10, v.y);
+    };
+    st_fp(F + R_ZERO * 10, zero);
+    st_fp(F + R_ONE * 10, one);
+    st_fp(F + R_PX * 10, C.hx);
+    st_fp(F + R_PY * 10, C.hy);
+    st_fp(F + R_SX * 10, C.sx);
+    st_fp(F + R_NSY * 10, nsy);
+    put2(R_X_x, C.qx);
+    put2(R_Y_x, C.qy);
+    put2(R_Z_x, one2);
+    put2(R_T_x, one2);
+    put2(R_QX_x, C.qx);
+    put2(R_QY_x, C.qy);
+    put2(R_NQY_x, nqy);
+    put2(R_R2_x, r2);
+    put2(R_P1X_x, q1x);
+    put2(R_P1Y_x, q1y);
+    put2(R_P1R2_x, q1r2);
+    put2(R_P2X_x, q2x);
+    put2(R_F2ONE_x, one2);
+    put2(R_F2ZERO_x, zero2);
   }
+  team_sync();
 }
+
+// Loads the G2Base line s (a, bx, cy: 6 Fp) into FA, FBX, FCY.
+HG_DEV void load_fixed_line(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
+  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
+  if (T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
+  team_sync();
+}
+
+// f *= pk line (LA, LB, LC) and, when has_fixed, the G2Base line (FA, FB, FC).
+// A point at infinity contributes the unit line (a = b = 0, c = 1); the choice
+// is an address select, so teams of one wave stay convergent.
+HG_DEV void apply_lines(const Team& T, const uint32_t* F, const CheckCtx& C, bool has_fixed) {
+  t12_mul_line_regs(T, S_F, S_F, F, C.use_q ? R_LA_x : R_F2ZERO_x, C.use_q ? R_LB_x : R_F2ZERO_x,
+                    C.use_q ? R_LC_x : R_F2ONE_x);
+  if (has_fixed)
+    t12_mul_line_regs(T, S_F, S_F, F, C.use_s ? R_FA_x : R_F2ZERO_x, C.use_s ? R_FB_x : R_F2ZERO_x,
+                      C.use_s ? R_FC_x : R_F2ONE_x);
+}
+
+// f = Miller(pk at H) * Miller(G2Base at -sig) (x/crypto optate.go miller, with
+// the two loops sharing their squarings); the G2 steps run as team programs.
+HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, const LineCoef* tab, bool has_fixed) {
+  const int8_t naf[kNafLen] = HG_NAF;
+  t12_set_one(T, S_F);
+  g2_regs_init(T, F, C);
+  int s = 0;
+  for (int i = kNafLen - 1; i > 0; i--) {
+    load_fixed_line(T, F, tab, s++);
+    g2_program(T, F, kProgDBL);
+    if (i != kNafLen - 1) t12_sqr(T, S_F, S_F);
+    apply_lines(T, F, C, has_fixed);
+    int d = naf[i - 1];
+    if (d != 0) {
+      load_fixed_line(T, F, tab, s++);
+      if (d > 0) g2_program(T, F, kProgADD_POS);
+      else g2_program(T, F, kProgADD_NEG);
+      apply_lines(T, F, C, has_fixed);
+    }
+  }
+  load_fixed_line(T, F, tab, s++);
+  g2_program(T, F, kProgADD_F1);
+  apply_lines(T, F, C, has_fixed);
+  load_fixed_line(T, F, tab, s++);
+  g2_program(T, F, kProgADD_F2);
+  apply_lines(T, F, C, has_fixed);
+}
+
+HG_DEV uint32_t* team_regs(const Team& T) { return T.base + kSlots * kFp12Words; }
 
 __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const LineCoef* tab,
                                                const PointG1* hpt, int32_t* codes) {
   __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
   Team T = make_team(lds, kTeamWords);
+  uint32_t* F = team_regs(T);
   int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
   bool valid = idx < n;
   int ci = valid ? idx : n - 1;
@@ -356,22 +386,18 @@ __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const L
   CheckCtx C;
   C.qx = I.pk.x;
   C.qy = I.pk.y;
-  f2_neg(C.nqy, C.qy);
-  f2_sqr(C.r2, C.qy);
   C.hx = hpt->x;
   C.hy = hpt->y;
   C.sx = I.sig.x;
-  fp_neg(C.nsy, I.sig.y);
+  C.sy = I.sig.y;
   C.use_q = I.pk.inf == 0;
   C.use_s = I.sig.inf == 0;
   if (!C.use_q) {  // keep the (unused) doubling chain well-defined
     const Fp2 gx = HG_G2X, gy = HG_G2Y;
     C.qx = gx;
     C.qy = gy;
-    f2_neg(C.nqy, C.qy);
-    f2_sqr(C.r2, C.qy);
   }
-  team_miller_check(T, C, tab, true);
+  team_miller_check(T, F, C, tab, true);
   team_final_exp(T);
   bool ok = t12_is_one(T, S_F);
   if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
@@ -382,6 +408,7 @@ __global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* 
                                              uint8_t* gt_out) {
   __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
   Team T = make_team(lds, kTeamWords);
+  uint32_t* F = team_regs(T);
   int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
   bool valid = idx < n;
   int ci = valid ? idx : n - 1;
@@ -400,13 +427,11 @@ __global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* 
   }
   C.qx = Q.x;
   C.qy = Q.y;
-  f2_neg(C.nqy, C.qy);
-  f2_sqr(C.r2, C.qy);
   C.hx = P.x;
   C.hy = P.y;
   fp_zero(C.sx);
-  fp_zero(C.nsy);
-  team_miller_check(T, C, tab, false);
+  fp_zero(C.sy);
+  team_miller_check(T, F, C, tab, false);
   team_final_exp(T);  // f == 1 when either input is infinity, and 1^e == 1
   // GT.Marshal order: coefficients 5,3,1,4,2,0, each as (x, y)
   if (valid && T.active) {
