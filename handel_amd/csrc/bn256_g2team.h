@@ -53,13 +53,20 @@ HG_DEV void acc_reduce8(Fp& r, Acc& a) {
 // sum_m c_m * F[r_m] + K p  (K = sum of the negative |c_m|): a non-negative
 // value < (sum |c_m|) p with normalized limbs. Coefficients are small
 // (|sum| <= 24, checked by the generator), so limb sums fit in int32.
-HG_DEV void g2_lincomb(Fp& out, const uint32_t* F, const uint8_t* rr, const int8_t* cc, int nt) {
+// Operand address: F register (< 128), element of Fp12 slot A (128..139) or B (160..171).
+HG_DEV const uint32_t* op_addr(const uint32_t* F, const uint32_t* A, const uint32_t* B, uint32_t r) {
+  const uint32_t* base = (r & 128u) ? ((r & 32u) ? B : A) : F;
+  return base + (r & 31u) * 10 + ((r & 128u) ? 0u : (r & 96u) * 10);
+}
+
+HG_DEV void g2_lincomb(Fp& out, const uint32_t* F, const uint32_t* A, const uint32_t* B, const uint8_t* rr,
+                       const int8_t* cc, int nt) {
   int32_t v[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) v[i] = 0;
   int32_t negk = 0;
   for (int m = 0; m < nt; m++) {
-    const uint32_t* x = F + rr[m] * 10;
+    const uint32_t* x = op_addr(F, A, B, rr[m]);
     int32_t k = cc[m];
     negk += k < 0 ? -k : 0;
 #pragma unroll
@@ -74,31 +81,52 @@ HG_DEV void g2_lincomb(Fp& out, const uint32_t* F, const uint8_t* rr, const int8
   }
 }
 
-HG_DEV void g2_round(const Team& T, uint32_t* F, const G2Round& R) {
+// One round: every lane computes its dst = sum_slot lincomb_a * lincomb_b.
+// A, B: Fp12 source slots; D: Fp12 destination slot (dst codes >= 128).
+HG_DEV void g2_round(const Team& T, uint32_t* F, const uint32_t* A, const uint32_t* B, uint32_t* D,
+                     const G2Round& R) {
   const G2Lane& L = kG2Lanes[R.first + T.tl];
   Acc acc;
   acc_zero(acc);
 #pragma unroll
-  for (int s = 0; s < 3; s++) {
+  for (int s = 0; s < kG2MaxSlots; s++) {
     if (s < R.nslot) {
       Fp a, b;
-      g2_lincomb(a, F, L.ar[s], L.ac[s], R.nta[s]);
-      g2_lincomb(b, F, L.br[s], L.bc[s], R.ntb[s]);
+      g2_lincomb(a, F, A, B, L.ar[s], L.ac[s], R.nta[s]);
+      g2_lincomb(b, F, A, B, L.br[s], L.bc[s], R.ntb[s]);
       acc_mad(acc, a, b);
     }
   }
   Fp r;
   acc_reduce8(r, acc);
-  uint8_t dst = L.dst;
+  uint32_t dst = L.dst;
   team_sync();
-  if (dst != kG2None) st_fp(F + dst * 10, r);
+  if (dst != kG2None) st_fp(((dst & 128u) ? D + (dst & 31u) * 10 : F + dst * 10), r);
   team_sync();
 }
 
 template <int N>
 HG_DEV void g2_program(const Team& T, uint32_t* F, const G2Round (&prog)[N]) {
 #pragma unroll
-  for (int i = 0; i < N; i++) g2_round(T, F, prog[i]);
+  for (int i = 0; i < N; i++) g2_round(T, F, F, F, F, prog[i]);
+}
+
+// Fp12 squaring of slot sa into slot dst (symmetric products merged, 7 slots per lane)
+HG_DEV void t12_sqr_fast(const Team& T, uint32_t* F, int dst, int sa) {
+  g2_round(T, F, slot(T, sa), slot(T, sa), slot(T, dst), kProgSQR12[0]);
+}
+// Granger-Scott squaring, valid for elements of the cyclotomic subgroup
+// (everything after the easy part of the final exponentiation)
+HG_DEV void t12_cyc_sqr(const Team& T, uint32_t* F, int dst, int sa) {
+  g2_round(T, F, slot(T, sa), slot(T, sa), slot(T, dst), kProgCYC_SQR[0]);
+}
+// dst = a^u with cyclotomic squarings (x/crypto gfP12.Exp(t, u)), dst != sa
+HG_DEV void t12_pow_u_cyc(const Team& T, uint32_t* F, int dst, int sa) {
+  t12_copy(T, dst, sa);
+  for (int bit = 61; bit >= 0; bit--) {
+    t12_cyc_sqr(T, F, dst, dst);
+    if ((kU >> bit) & 1) t12_mul(T, dst, dst, sa);
+  }
 }
 
 // dst = a * (c + b w + a3 w^3) with the line coefficients in the register

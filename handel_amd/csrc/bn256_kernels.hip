@@ -227,7 +227,7 @@ static constexpr int kTeamWords = kSlots * kFp12Words + kG2Regs * 10;
 static constexpr int kTeamsPerBlock = 4;
 
 // the pairing's final exponentiation (x/crypto optate.go finalExponentiation)
-HG_DEV void team_final_exp(const Team& T) {
+HG_DEV void team_final_exp(const Team& T, uint32_t* F) {
   t12_inv(T, S_A, S_F, S_K, S_L);  // A = f^-1
   t12_conj(T, S_B, S_F);           // B = conj(f)
   t12_mul(T, S_F, S_B, S_A);       // t1 = f^(p^6 - 1)
@@ -238,9 +238,9 @@ HG_DEV void team_final_exp(const Team& T) {
   t12_mul(T, S_A, S_A, S_B);
   t12_frob(T, S_B, S_B);           // fp3
   t12_mul(T, S_A, S_A, S_B);       // y0 = fp * fp2 * fp3
-  t12_pow_u(T, S_C, S_F);          // fu
-  t12_pow_u(T, S_D, S_C);          // fu2
-  t12_pow_u(T, S_E, S_D);          // fu3
+  t12_pow_u_cyc(T, F, S_C, S_F);          // fu
+  t12_pow_u_cyc(T, F, S_D, S_C);          // fu2
+  t12_pow_u_cyc(T, F, S_E, S_D);          // fu3
   t12_frob(T, S_G, S_C);
   t12_conj(T, S_G, S_G);           // y3 = conj(frob(fu))
   t12_frob(T, S_H, S_D);
@@ -251,19 +251,19 @@ HG_DEV void team_final_exp(const Team& T) {
   t12_frob(T, S_I, S_E);
   t12_mul(T, S_I, S_E, S_I);
   t12_conj(T, S_I, S_I);           // y6 = conj(fu3 * frob(fu3))
-  t12_sqr(T, S_K, S_I);
+  t12_cyc_sqr(T, F, S_K, S_I);
   t12_mul(T, S_K, S_K, S_H);
   t12_mul(T, S_K, S_K, S_D);       // t0 = y6^2 y4 y5
   t12_mul(T, S_J, S_G, S_D);
   t12_mul(T, S_J, S_J, S_K);       // t1 = y3 y5 t0
   t12_mul(T, S_K, S_K, S_C);       // t0 = t0 y2
-  t12_sqr(T, S_J, S_J);
+  t12_cyc_sqr(T, F, S_J, S_J);
   t12_mul(T, S_J, S_J, S_K);
-  t12_sqr(T, S_J, S_J);            // t1 = (t1^2 t0)^2
+  t12_cyc_sqr(T, F, S_J, S_J);            // t1 = (t1^2 t0)^2
   t12_conj(T, S_L, S_F);           // y1 = conj(t1_easy)
   t12_mul(T, S_K, S_J, S_L);       // t0 = t1 y1
   t12_mul(T, S_J, S_J, S_A);       // t1 = t1 y0
-  t12_sqr(T, S_K, S_K);
+  t12_cyc_sqr(T, F, S_K, S_K);
   t12_mul(T, S_F, S_K, S_J);       // result
 }
 
@@ -354,7 +354,7 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   for (int i = kNafLen - 1; i > 0; i--) {
     load_fixed_line(T, F, tab, s++);
     g2_program(T, F, kProgDBL);
-    if (i != kNafLen - 1) t12_sqr(T, S_F, S_F);
+    if (i != kNafLen - 1) t12_sqr_fast(T, F, S_F, S_F);
     apply_lines(T, F, C, has_fixed);
     int d = naf[i - 1];
     if (d != 0) {
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const L
     C.qy = gy;
   }
   team_miller_check(T, F, C, tab, true);
-  team_final_exp(T);
+  team_final_exp(T, F);
   bool ok = t12_is_one(T, S_F);
   if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
 }
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* 
   fp_zero(C.sx);
   fp_zero(C.sy);
   team_miller_check(T, F, C, tab, false);
-  team_final_exp(T);  // f == 1 when either input is infinity, and 1^e == 1
+  team_final_exp(T, F);  // f == 1 when either input is infinity, and 1^e == 1
   // GT.Marshal order: coefficients 5,3,1,4,2,0, each as (x, y)
   if (valid && T.active) {
     const int pos[6] = {5, 2, 4, 1, 3, 0};  // position of coefficient k in the marshal

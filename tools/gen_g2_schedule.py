@@ -1,19 +1,30 @@
 #!/usr/bin/env python3
-"""Generates handel_amd/csrc/bn256_g2sched.h: the lane-parallel schedule of the
-Miller loop's G2 steps (x/crypto optate.go lineFunctionDouble /
-lineFunctionAdd) for a 16-lane team.
+"""Generates handel_amd/csrc/bn256_g2sched.h: lane-parallel "team programs"
+for a 16-lane team (bn256_g2team.h executes them).
 
-A *program* is a short list of rounds. In a round every lane of the team
+A program is a short list of rounds. In a round every lane of the team
 computes one Fp element
-    dst = sum_{slot} (sum_m ca_m * F[ra_m]) * (sum_m cb_m * F[rb_m])
-over the team's LDS register file F (Fp elements in Montgomery form), with
-small signed integer coefficients, then stores it. All lanes run the same
-instruction stream (only addresses and coefficients differ), rounds are
-separated by a team barrier. The tables are validated here by interpreting
-them with plain modular arithmetic against the oracle's line functions
-(tests/test_g2_schedule.py runs the same check in the CPU suite).
+    dst = sum_{slot} (sum_m ca_m * X[ra_m]) * (sum_m cb_m * X[rb_m])
+with small signed integer coefficients and ONE lazy Montgomery reduction,
+then stores it; all lanes run the same instruction stream (only addresses
+and coefficients differ), rounds are separated by a team barrier (every
+lane reads before any lane writes, so in-place programs are fine).
 
-Build tooling only: nothing in the product imports this file.
+Operand index space (uint8):
+    0..127    the team's LDS register file F (Fp elements)
+    128..139  element e of the program's Fp12 source slot A (2k + c)
+    160..171  element e of the program's Fp12 source slot B
+Destination: an F register (< 128), element e of the destination Fp12
+slot (128 + e), or 255 (lane idle).
+
+Programs:
+    DBL, ADD_*     x/crypto optate.go lineFunctionDouble / lineFunctionAdd
+    CYC_SQR        Granger-Scott squaring in the cyclotomic subgroup
+                   (final exponentiation: gfP12.Exp(.., u) squarings)
+    SQR12          Fp12 squaring with the symmetric products merged
+The tables are validated here by interpreting them with plain modular
+arithmetic against the oracle (tests/test_g2_schedule.py repeats this in
+the CPU suite). Build tooling only: nothing in the product imports it.
 """
 
 from __future__ import annotations
@@ -23,10 +34,12 @@ import random
 import sys
 
 P = 65000549695646603732796438742359905742825358107623003571877145026864184071783
-# R/p for the 10 x 26-bit Montgomery representation: REDC(T) < T/R + p
-R_OVER_P = (1 << 260) / P
-MAX_NSLOT = 3
+R_OVER_P = (1 << 260) / P  # REDC(T) < T/R + p
+MAX_NSLOT = 7
 MAX_TERMS = 6
+SLOT_A = 128
+SLOT_B = 160
+NONE = 255
 
 # ------------------------------------------------------------------ register file
 FP_SCALARS = ["ZERO", "ONE", "PX", "PY", "SX", "NSY"]
@@ -44,7 +57,13 @@ for i, n in enumerate(FP2_REGS):
     REG[n + ".x"] = _base + 2 * i
     REG[n + ".y"] = _base + 2 * i + 1
 NREGS = _base + 2 * len(FP2_REGS)
-NONE = 255
+assert NREGS <= 128
+# Fp12 source slots: Fp2 coefficient k of slot A is "A{k}", of slot B "B{k}"
+for k in range(6):
+    for ci, c in enumerate("xy"):
+        REG[f"A{k}.{c}"] = SLOT_A + 2 * k + ci
+        REG[f"B{k}.{c}"] = SLOT_B + 2 * k + ci
+        REG[f"D{k}.{c}"] = SLOT_A + 2 * k + ci  # destination slot element (same encoding)
 
 
 def comp(name, c):
@@ -52,7 +71,7 @@ def comp(name, c):
 
 
 # ------------------------------------------------------------------ expression helpers
-# An Fp2 linear combination is a list of (fp2_name, coef). Its component c is
+# An Fp2 linear combination is a list of (fp2_name, coef); its component c is
 # the Fp lincomb [(reg(name.c), coef)].
 def fp2_comp(lc, c):
     return [(comp(n, c), k) for n, k in lc]
@@ -60,6 +79,10 @@ def fp2_comp(lc, c):
 
 def neg(terms):
     return [(r, -k) for r, k in terms]
+
+
+def scale(terms, s):
+    return [(r, k * s) for r, k in terms]
 
 
 def add(*ts):
@@ -119,6 +142,31 @@ def lin(dst, U):
     return [Lane(comp(dst, c), [(fp2_comp(U, c), one())]) for c in ("x", "y")]
 
 
+# Fp-level product terms of Fp2 expressions, for building sums per component.
+def prod_terms(U, V, c, k=1):
+    """component c of k * U * V as a list of Fp slots."""
+    ux, uy = fp2_comp(U, "x"), fp2_comp(U, "y")
+    vx, vy = fp2_comp(V, "x"), fp2_comp(V, "y")
+    if c == "x":
+        return [(scale(ux, k), vy), (scale(uy, k), vx)]
+    return [(scale(uy, k), vy), (scale(neg(ux), k), vx)]
+
+
+def sq_terms(U, c, k=1):
+    ux, uy = fp2_comp(U, "x"), fp2_comp(U, "y")
+    if c == "x":
+        return [(scale(add(ux, ux), k), uy)]
+    return [(scale(add(uy, ux), k), add(uy, neg(ux)))]
+
+
+def xi_terms(slots_x, slots_y, c):
+    """component c of xi * Z where Z = (sum slots_x, sum slots_y):
+    xi Z = (3 Zx + Zy) i + (3 Zy - Zx)."""
+    if c == "x":
+        return [(scale(a, 3), b) for a, b in slots_x] + list(slots_y)
+    return [(scale(a, 3), b) for a, b in slots_y] + [(neg(a), b) for a, b in slots_x]
+
+
 # ------------------------------------------------------------------ programs
 def fixed_line_eval():
     # FB = FBX * SX, FC = FCY * NSY  (the G2Base line at -sig)
@@ -163,12 +211,74 @@ def prog_add(px, py, pr2):
     return [a1, a2, a3, a4, a5]
 
 
+def prog_cyc_sqr():
+    """Granger-Scott squaring of f = (c0 + c3 s) + (c1 + c4 s) w + (c2 + c5 s) w^2
+    (s = w^3, s^2 = xi) in the cyclotomic subgroup:
+        A^2 = (a^2 + xi b^2) + ((a + b)^2 - a^2 - b^2) s = (a^2 + xi b^2) + 2ab s
+        c0' = 3 (A^2)_0 - 2 c0      c3' = 3 (A^2)_1 + 2 c3        (A = (c0, c3))
+        c2' = 3 (B^2)_0 - 2 c2      c5' = 3 (B^2)_1 + 2 c5        (B = (c1, c4))
+        c1' = 3 xi (C^2)_1 + 2 c1   c4' = 3 (C^2)_0 - 2 c4        (C = (c2, c5))"""
+    lanes = []
+
+    def a0(a, b, c):  # component c of 3 (a^2 + xi b^2)
+        bx = sq_terms([(b, 1)], "x")
+        by = sq_terms([(b, 1)], "y")
+        return [(scale(x, 3), y) for x, y in sq_terms([(a, 1)], c) + xi_terms(bx, by, c)]
+
+    def a1(a, b, c, k=3):  # component c of k * 2ab
+        return prod_terms([(a, 2 * k)], [(b, 1)], c)
+
+    for c in "xy":
+        lanes.append(Lane(comp("D0", c), a0("A0", "A3", c) + [(fp2_comp([("A0", -2)], c), one())]))
+        lanes.append(Lane(comp("D3", c), a1("A0", "A3", c) + [(fp2_comp([("A3", 2)], c), one())]))
+        lanes.append(Lane(comp("D2", c), a0("A1", "A4", c) + [(fp2_comp([("A2", -2)], c), one())]))
+        lanes.append(Lane(comp("D5", c), a1("A1", "A4", c) + [(fp2_comp([("A5", 2)], c), one())]))
+        lanes.append(Lane(comp("D4", c), a0("A2", "A5", c) + [(fp2_comp([("A4", -2)], c), one())]))
+        # 3 xi (C^2)_1 = xi * 6 c2 c5
+        px = prod_terms([("A2", 6)], [("A5", 1)], "x")
+        py = prod_terms([("A2", 6)], [("A5", 1)], "y")
+        lanes.append(Lane(comp("D1", c), xi_terms(px, py, c) + [(fp2_comp([("A1", 2)], c), one())]))
+    return [lanes]
+
+
+def prog_sqr12():
+    """f^2 in Fp2[w]/(w^6 - xi): c_k = sum_{i<=j, i+j = k mod 6} (2 - [i==j]) a_i a_j xi^[i+j>=6]."""
+    def xi_prod(i, j, c, mult):
+        # component c of mult * (xi a_i) * a_j, xi a = (3x + y) i + (3y - x)
+        ux = [(comp(f"A{i}", "x"), 3 * mult), (comp(f"A{i}", "y"), mult)]
+        uy = [(comp(f"A{i}", "y"), 3 * mult), (comp(f"A{i}", "x"), -mult)]
+        vx, vy = [(comp(f"A{j}", "x"), 1)], [(comp(f"A{j}", "y"), 1)]
+        if c == "x":
+            return [(ux, vy), (uy, vx)]
+        return [(uy, vy), (neg(ux), vx)]
+
+    lanes = []
+    for k in range(6):
+        for c in "xy":
+            slots = []
+            for i in range(6):
+                for j in range(i, 6):
+                    if (i + j) % 6 != k:
+                        continue
+                    mult = 1 if i == j else 2
+                    if i + j >= 6:
+                        slots += xi_prod(i, j, c, mult)
+                    elif i == j:
+                        slots += sq_terms([(f"A{i}", 1)], c)
+                    else:
+                        slots += prod_terms([(f"A{i}", mult)], [(f"A{j}", 1)], c)
+            lanes.append(Lane(comp(f"D{k}", c), slots))
+    return [lanes]
+
+
 PROGRAMS = {
     "DBL": prog_double(),
     "ADD_POS": prog_add("QX", "QY", "R2"),
     "ADD_NEG": prog_add("QX", "NQY", "R2"),
     "ADD_F1": prog_add("P1X", "P1Y", "P1R2"),
     "ADD_F2": prog_add("P2X", "QY", "R2"),
+    "CYC_SQR": prog_cyc_sqr(),
+    "SQR12": prog_sqr12(),
 }
 
 
@@ -181,25 +291,27 @@ def check_round(lanes, name):
     assert len(lanes) <= 16, f"{name}: {len(lanes)} lanes"
     dsts = [l.dst for l in lanes]
     assert len(set(dsts)) == len(dsts), f"{name}: duplicate destinations"
-    total = 0
+    worst = 0
     for l in lanes:
-        assert len(l.slots) <= MAX_NSLOT, f"{name}: too many slots"
+        assert len(l.slots) <= MAX_NSLOT, f"{name}: {len(l.slots)} slots"
         t = 0
         for a, b in l.slots:
             assert len(a) <= MAX_TERMS and len(b) <= MAX_TERMS, f"{name}: too many terms {a} {b}"
+            # int32 limb sums in g2_lincomb: |v + K p_i| <= (pos + neg) * 2^26 < 2^31
+            for terms in (a, b):
+                pos = sum(k for _, k in terms if k > 0)
+                negs = sum(-k for _, k in terms if k < 0)
+                assert pos + negs <= 30, f"{name}: coefficient range {terms}"
             t += bound(a) * bound(b)
         # REDC output < (t / R_OVER_P + 1) p must stay below 8p (fp_reduce8)
         assert t / R_OVER_P + 1 < 8, f"{name}: product bound {t}"
-        total = max(total, t)
-    # a round must not read a register another lane of the same round writes
-    reads = {r for l in lanes for a, b in l.slots for r, _ in a + b}
-    clash = reads & set(dsts)
-    assert not clash, f"{name}: read/write clash on {[k for k, v in REG.items() if v in clash]}"
-    return total
+        # 64-bit columns: limbs < 2^26 * sum|c|; 10 terms per column per slot
+        worst = max(worst, t)
+    return worst
 
 
 def run_program(prog, F):
-    """Interprets a program on a register file of plain residues mod p."""
+    """Interprets a program on an index -> residue map (plain values mod p)."""
     for lanes in prog:
         out = {}
         for l in lanes:
@@ -221,21 +333,19 @@ def validate(seed=1):
     for name, prog in PROGRAMS.items():
         for i, r in enumerate(prog):
             check_round(r, f"{name}[{i}]")
-    for trial in range(4):
+    for trial in range(3):
         Q = O.g2_mul(O.G2_GEN, rng.randrange(1, O.ORDER))
         Hp = O.g1_mul(O.G1_GEN, rng.randrange(1, O.ORDER))
         Rj = O.jac_mul(O.FP2_OPS, O.to_jac(O.FP2_OPS, Q), rng.randrange(2, 1000))
         r = (Rj[0], Rj[1], Rj[2], O.f2_sqr(Rj[2]))
-        F = {i: rng.randrange(P) for i in range(NREGS)}
+        F = {i: rng.randrange(P) for i in list(range(NREGS)) + list(range(SLOT_A, SLOT_A + 12))
+             + list(range(SLOT_B, SLOT_B + 12))}
         F[REG["ZERO"]] = 0
         F[REG["ONE"]] = 1
         F[REG["PX"]], F[REG["PY"]] = Hp
 
         def put(n, v):
             F[comp(n, "x")], F[comp(n, "y")] = v
-
-        def get(n):
-            return (F[comp(n, "x")], F[comp(n, "y")])
 
         for n, v in zip(("X", "Y", "Z", "T"), r):
             put(n, v)
@@ -246,42 +356,54 @@ def validate(seed=1):
         a, b, c, r_new = O._line_double(r, *Hp)
         G = run_program(PROGRAMS["DBL"], dict(F))
         assert [(G[comp(n, "x")], G[comp(n, "y")]) for n in ("X", "Y", "Z", "T")] == list(r_new), "DBL point"
-        assert (G[comp("LA", "x")], G[comp("LA", "y")]) == a, "DBL a"
-        assert (G[comp("LB", "x")], G[comp("LB", "y")]) == b, "DBL b"
-        assert (G[comp("LC", "x")], G[comp("LC", "y")]) == c, "DBL c"
+        assert [(G[comp(n, "x")], G[comp(n, "y")]) for n in ("LA", "LB", "LC")] == [a, b, c], "DBL line"
         for prog, pq in (("ADD_POS", (Q[0], Q[1])), ("ADD_NEG", (Q[0], O.f2_neg(Q[1])))):
             a, b, c, r_new = O._line_add(r, pq, *Hp, O.f2_sqr(pq[1]))
             G = run_program(PROGRAMS[prog], dict(F))
             assert [(G[comp(n, "x")], G[comp(n, "y")]) for n in ("X", "Y", "Z", "T")] == list(r_new), prog
             assert [(G[comp(n, "x")], G[comp(n, "y")]) for n in ("LA", "LB", "LC")] == [a, b, c], prog + " line"
+        # Fp12 squarings: a random element, and a cyclotomic one
+        f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+        cyc = O.f12_mul(O.f12_conj(f), O.f12_inv(f))
+        cyc = O.f12_mul(cyc, O.f12_frob2(cyc))
+        for prog, val in (("SQR12", f), ("CYC_SQR", cyc)):
+            G = dict(F)
+            for k in range(6):
+                G[comp(f"A{k}", "x")], G[comp(f"A{k}", "y")] = val[k]
+            G = run_program(PROGRAMS[prog], G)
+            got = [(G[comp(f"D{k}", "x")], G[comp(f"D{k}", "y")]) for k in range(6)]
+            assert got == O.f12_sqr(val), prog
     return True
 
 
 # ------------------------------------------------------------------ emit
 def emit(path):
     lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
-             "// Lane-parallel schedule of the Miller loop's G2 steps (see the generator).",
+             "// Lane-parallel team programs (see the generator for the encoding).",
              "#pragma once", "#include <stdint.h>", "namespace hg {",
              f"static constexpr int kG2Regs = {NREGS};", f"static constexpr int kG2MaxSlots = {MAX_NSLOT};",
-             f"static constexpr int kG2MaxTerms = {MAX_TERMS};", f"static constexpr uint8_t kG2None = {NONE};"]
+             f"static constexpr int kG2MaxTerms = {MAX_TERMS};", f"static constexpr uint8_t kG2None = {NONE};",
+             f"static constexpr int kOpSlotA = {SLOT_A};", f"static constexpr int kOpSlotB = {SLOT_B};"]
     for k, v in REG.items():
-        lines.append(f"static constexpr int R_{k.replace('.', '_')} = {v};")
-    lines.append("struct G2Lane {\n  uint8_t dst, pad[3];\n  uint8_t ar[3][6];\n  int8_t ac[3][6];\n"
-                 "  uint8_t br[3][6];\n  int8_t bc[3][6];\n};")
-    lines.append("struct G2Round {\n  int nslot, nta[3], ntb[3], first;  // first = index into kG2Lanes\n};")
+        if v < 128:
+            lines.append(f"static constexpr int R_{k.replace('.', '_')} = {v};")
+    lines.append(f"struct G2Lane {{\n  uint8_t dst, pad[3];\n  uint8_t ar[{MAX_NSLOT}][{MAX_TERMS}];\n"
+                 f"  int8_t ac[{MAX_NSLOT}][{MAX_TERMS}];\n  uint8_t br[{MAX_NSLOT}][{MAX_TERMS}];\n"
+                 f"  int8_t bc[{MAX_NSLOT}][{MAX_TERMS}];\n}};")
+    lines.append(f"struct G2Round {{\n  int nslot, nta[{MAX_NSLOT}], ntb[{MAX_NSLOT}], first;  // first = index into kG2Lanes\n}};")
     all_lanes = []
     rounds = {}
     for name, prog in PROGRAMS.items():
         rounds[name] = []
         for r in prog:
             nslot = max(len(l.slots) for l in r)
-            nta = [max((len(l.slots[s][0]) if s < len(l.slots) else 0) for l in r) for s in range(3)]
-            ntb = [max((len(l.slots[s][1]) if s < len(l.slots) else 0) for l in r) for s in range(3)]
+            nta = [max((len(l.slots[s][0]) if s < len(l.slots) else 0) for l in r) for s in range(MAX_NSLOT)]
+            ntb = [max((len(l.slots[s][1]) if s < len(l.slots) else 0) for l in r) for s in range(MAX_NSLOT)]
             rounds[name].append((nslot, nta, ntb, len(all_lanes)))
             for t in range(16):
                 l = r[t] if t < len(r) else None
                 ent = {"dst": l.dst if l else NONE, "ar": [], "ac": [], "br": [], "bc": []}
-                for s in range(3):
+                for s in range(MAX_NSLOT):
                     a, b = (l.slots[s] if (l and s < len(l.slots)) else ([], []))
                     pa = list(a) + [(REG["ZERO"], 0)] * (MAX_TERMS - len(a))
                     pb = list(b) + [(REG["ZERO"], 0)] * (MAX_TERMS - len(b))
@@ -299,7 +421,7 @@ def emit(path):
         lines.append(f"  {{{e['dst']}, {{0, 0, 0}}, {arr(e['ar'])}, {arr(e['ac'])}, {arr(e['br'])}, {arr(e['bc'])}}},")
     lines.append("};")
     for name, rs in rounds.items():
-        body = ", ".join(f"{{{n}, {{{a[0]}, {a[1]}, {a[2]}}}, {{{b[0]}, {b[1]}, {b[2]}}}, {f}}}" for n, a, b, f in rs)
+        body = ", ".join(f"{{{n}, {arr(a)}, {arr(b)}, {f}}}" for n, a, b, f in rs)
         lines.append(f"static constexpr int kProg{name}Len = {len(rs)};")
         lines.append(f"static constexpr G2Round kProg{name}[{len(rs)}] = {{{body}}};")
     lines.append("}  // namespace hg")
