@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+from handel_amd.distributed import gather_verdicts, pack_verdicts  # noqa: E402
 from handel_amd.engine import Engine  # noqa: E402
 
 LIB_MESSAGE = b"Everything that is beautiful and noble is the product of reason and calculation."
@@ -122,20 +123,13 @@ def main():
     d_pks = torch.frombuffer(bytearray(pks), dtype=torch.uint8).to(dev)
     d_sigs = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
     d_codes = torch.zeros(n, dtype=torch.int32, device=dev)
-    nbits = (n + 7) // 8 * 8
-    weights = (2 ** torch.arange(8, device=dev, dtype=torch.int32)).view(1, 8)
-    gathered = [torch.zeros(nbits // 8, dtype=torch.uint8, device=dev) for _ in range(world)]
+    gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev) for _ in range(world)]
     stream = torch.cuda.current_stream(dev)
 
     def step():
         eng.verify_batch_device(d_pks.data_ptr(), d_sigs.data_ptr(), n, d_codes.data_ptr(), stream.cuda_stream)
-        ok = torch.zeros(nbits, dtype=torch.int32, device=dev)
-        ok[:n] = (d_codes == 0).to(torch.int32)
-        bits = (ok.view(-1, 8) * weights).sum(dim=1).to(torch.uint8)  # verdict bitset (bit i = check i valid)
-        if dist:
-            tdist.all_gather(gathered, bits)
-        else:
-            gathered[0].copy_(bits)
+        # verdict bitset (bit i = check i valid), gathered over RCCL: the only cross-GPU traffic
+        gather_verdicts(pack_verdicts(d_codes), world, gathered)
 
     for _ in range(args.warmup):
         step()

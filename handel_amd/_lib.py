@@ -51,10 +51,13 @@ SIGNATURES = {
     "hg_verify_aggregate_device": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
     "hg_aggregate_pk": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P]),
     "hg_combine_g1": (_I, [_P, _P, _P, _SZ, _P, _P]),
+    "hg_combine_g2": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "hg_pair": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "hg_keygen": (_I, [_P, _P, _SZ, _P]),
     "hg_sign": (_I, [_P, _P, _SZ, _P]),
     "hg_debug_fp_mul": (_I, [_P, _P, _P, _SZ, _P]),
+    "hg_diag_read": (_I, [_P, _P, _SZ]),
+    "hg_debug_fp12": (_I, [_P, _I, _P, _P, _SZ, _P]),
     "hg_timing_enable": (_I, [_P, _I]),
     "hg_timing_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
     "hg_sync": (_I, [_P]),
@@ -71,7 +74,8 @@ def load(build_if_missing: bool = True):
     with _lock:
         if _lib is not None:
             return _lib
-        path = _build.LIB
+        # HG_LIB selects the diagnostic build (tools/diag.py); default: the product library
+        path = os.environ.get("HG_LIB") or _build.LIB
         if not os.path.exists(path):
             if not build_if_missing:
                 raise HandelGPUError(f"HIP library not built: {path}")

@@ -2,7 +2,9 @@
 
 hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU
 container (``__graft_entry__.build()``) and the resulting .so travels to the
-GPU box with the repo snapshot.
+GPU box with the repo snapshot. ``diag=True`` builds the separate
+diagnostic variant (-DHG_DIAG: in-kernel s_memtime phase counters) used only
+by tools/diag.py.
 """
 
 from __future__ import annotations
@@ -16,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libhandel_gpu.so")
+DIAG_LIB = os.path.join(OUT_DIR, "libhandel_gpu_diag.so")
 SOURCES = ["bn256_kernels.hip", "hg_api.cpp"]
 HEADERS = ["bn256_fp.h", "bn256_curve.h", "bn256_team.h", "bn256_kernels.h", "bn256_constants.h",
            "bn256_g2team.h", "bn256_g2sched.h"]
@@ -31,21 +34,24 @@ def _inputs():
     return files
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+def up_to_date(lib: str = LIB) -> bool:
+    if not os.path.exists(lib):
         return False
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def build_library(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
-        return LIB
+def build_library(force: bool = False, verbose: bool = True, diag: bool = False) -> str:
+    lib = DIAG_LIB if diag else LIB
+    if not force and up_to_date(lib):
+        return lib
     os.makedirs(OUT_DIR, exist_ok=True)
+    suffix = "_diag" if diag else ""
+    extra = ["-DHG_DIAG=1"] if diag else []
 
     def compile_one(src):
-        obj = os.path.join(OUT_DIR, os.path.splitext(src)[0] + ".o")
-        cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(OUT_DIR, os.path.splitext(src)[0] + suffix + ".o")
+        cmd = [HIPCC, *CFLAGS, *extra, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
@@ -53,15 +59,14 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
 
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build_library(force="--force" in sys.argv)
-    print(LIB)
+    print(build_library(force="--force" in sys.argv, diag="--diag" in sys.argv))

@@ -15,40 +15,8 @@
 
 namespace hg {
 
-// Reduce a normalized-limb value < 8p (limb 9 holds the top bits) to [0, p).
-HG_DEV void fp_reduce8(Fp& r, const uint32_t* x) {
-  constexpr uint32_t p9 = p_top_limb();
-  uint32_t q = x[9] / (p9 + 1u);  // floor(value/p) - {0, 1}
-  uint32_t y[10];
-  int32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    int32_t v = (int32_t)x[i] - (int32_t)(q * p_limb(i)) + c;
-    y[i] = (i < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
-    c = v >> 26;
-  }
-  fp_csub(r, y);
-}
-
 // Montgomery REDC for T < ~199 p^2 (output < 8p), then full reduction.
-HG_DEV void acc_reduce8(Fp& r, Acc& a) {
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
-#pragma unroll
-    for (int j = 0; j < 10; j++) a.c[i + j] += (uint64_t)q * p_limb(j);
-    a.c[i + 1] += a.c[i] >> 26;
-  }
-  uint32_t x[10];
-  uint64_t carry = 0;
-#pragma unroll
-  for (int j = 0; j < 10; j++) {
-    uint64_t v = a.c[10 + j] + carry;
-    x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
-    carry = v >> 26;
-  }
-  fp_reduce8(r, x);
-}
+HG_DEV void acc_reduce8(Fp& r, Acc& a) { acc_reduce_wide(r, a); }
 
 // sum_m c_m * F[r_m] + K p  (K = sum of the negative |c_m|): a non-negative
 // value < (sum |c_m|) p with normalized limbs. Coefficients are small
@@ -111,20 +79,22 @@ HG_DEV void g2_program(const Team& T, uint32_t* F, const G2Round (&prog)[N]) {
   for (int i = 0; i < N; i++) g2_round(T, F, F, F, F, prog[i]);
 }
 
-// Fp12 squaring of slot sa into slot dst (symmetric products merged, 7 slots per lane)
-HG_DEV void t12_sqr_fast(const Team& T, uint32_t* F, int dst, int sa) {
+// The same Fp12 squarings as table programs (kProgSQR12 / kProgCYC_SQR); the
+// specialised index-arithmetic versions in bn256_team.h are what the kernels
+// run, these stay as a cross-check of the generated tables.
+HG_DEV void t12_sqr_table(const Team& T, uint32_t* F, int dst, int sa) {
   g2_round(T, F, slot(T, sa), slot(T, sa), slot(T, dst), kProgSQR12[0]);
 }
-// Granger-Scott squaring, valid for elements of the cyclotomic subgroup
-// (everything after the easy part of the final exponentiation)
-HG_DEV void t12_cyc_sqr(const Team& T, uint32_t* F, int dst, int sa) {
+HG_DEV void t12_cyc_sqr_table(const Team& T, uint32_t* F, int dst, int sa) {
   g2_round(T, F, slot(T, sa), slot(T, sa), slot(T, dst), kProgCYC_SQR[0]);
 }
+HG_DEV void t12_sqr_fast(const Team& T, uint32_t* F, int dst, int sa) { t12_sqr_fast(T, dst, sa); }
+HG_DEV void t12_cyc_sqr(const Team& T, uint32_t* F, int dst, int sa) { t12_cyc_sqr(T, dst, sa); }
 // dst = a^u with cyclotomic squarings (x/crypto gfP12.Exp(t, u)), dst != sa
 HG_DEV void t12_pow_u_cyc(const Team& T, uint32_t* F, int dst, int sa) {
   t12_copy(T, dst, sa);
   for (int bit = 61; bit >= 0; bit--) {
-    t12_cyc_sqr(T, F, dst, dst);
+    t12_cyc_sqr(T, dst, dst);
     if ((kU >> bit) & 1) t12_mul(T, dst, dst, sa);
   }
 }

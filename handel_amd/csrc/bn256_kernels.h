@@ -49,6 +49,9 @@ void launch_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, C
 void launch_merge_codes(const int32_t* a, const int32_t* b, int n, int32_t* out, hipStream_t s);
 void launch_sig_into_checks(const PointG1* sigs, int n, CheckIn* out, hipStream_t s);
 void launch_extract_pk(const CheckIn* in, int n, PointG2* out, hipStream_t s);
+int diag_read(uint64_t* out, size_t n);
+void launch_g2_combine(const PointG2* a, const PointG2* b, int n, PointG2* out, hipStream_t s);
+void launch_fp12_op(int op, const uint8_t* a, const uint8_t* b, int n, uint8_t* out, hipStream_t s);
 void launch_fp_mul(const uint32_t* a, const uint32_t* b, int n, uint32_t* out, hipStream_t s);
 
 }  // namespace hg

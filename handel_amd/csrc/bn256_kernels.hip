@@ -18,6 +18,24 @@
 
 namespace hg {
 
+// ------------------------------------------------------------------ diagnostics
+// Built only with -DHG_DIAG (tools/diag.py builds a separate library): lane 0
+// of every block accumulates s_memtime cycles per phase of k_verify.
+#ifdef HG_DIAG
+__shared__ uint64_t hg_diag_acc[16];
+__device__ uint64_t g_diag[4096 * 16];
+#define DIAG_T0() uint64_t diag_t0_ = __builtin_amdgcn_s_memtime()
+#define DIAG_ADD(k)                                                     \
+  do {                                                                  \
+    uint64_t diag_t1_ = __builtin_amdgcn_s_memtime();                   \
+    if (threadIdx.x == 0) hg_diag_acc[k] += diag_t1_ - diag_t0_;        \
+    diag_t0_ = diag_t1_;                                                \
+  } while (0)
+#else
+#define DIAG_T0() (void)0
+#define DIAG_ADD(k) (void)0
+#endif
+
 // ------------------------------------------------------------------ decode
 // Unmarshal rules:
 //   go (x/crypto): exact length checked by the host; coordinates taken mod p;
@@ -228,7 +246,9 @@ static constexpr int kTeamsPerBlock = 4;
 
 // the pairing's final exponentiation (x/crypto optate.go finalExponentiation)
 HG_DEV void team_final_exp(const Team& T, uint32_t* F) {
+  DIAG_T0();
   t12_inv(T, S_A, S_F, S_K, S_L);  // A = f^-1
+  DIAG_ADD(5);
   t12_conj(T, S_B, S_F);           // B = conj(f)
   t12_mul(T, S_F, S_B, S_A);       // t1 = f^(p^6 - 1)
   t12_frob2(T, S_A, S_F);
@@ -238,9 +258,11 @@ HG_DEV void team_final_exp(const Team& T, uint32_t* F) {
   t12_mul(T, S_A, S_A, S_B);
   t12_frob(T, S_B, S_B);           // fp3
   t12_mul(T, S_A, S_A, S_B);       // y0 = fp * fp2 * fp3
+  DIAG_ADD(6);
   t12_pow_u_cyc(T, F, S_C, S_F);          // fu
   t12_pow_u_cyc(T, F, S_D, S_C);          // fu2
   t12_pow_u_cyc(T, F, S_E, S_D);          // fu3
+  DIAG_ADD(7);
   t12_frob(T, S_G, S_C);
   t12_conj(T, S_G, S_G);           // y3 = conj(frob(fu))
   t12_frob(T, S_H, S_D);
@@ -265,6 +287,7 @@ HG_DEV void team_final_exp(const Team& T, uint32_t* F) {
   t12_mul(T, S_J, S_J, S_A);       // t1 = t1 y0
   t12_cyc_sqr(T, F, S_K, S_K);
   t12_mul(T, S_F, S_K, S_J);       // result
+  DIAG_ADD(6);
 }
 
 // Per-check inputs of the team Miller loop.
@@ -351,17 +374,25 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   t12_set_one(T, S_F);
   g2_regs_init(T, F, C);
   int s = 0;
+  DIAG_T0();
   for (int i = kNafLen - 1; i > 0; i--) {
     load_fixed_line(T, F, tab, s++);
+    DIAG_ADD(0);
     g2_program(T, F, kProgDBL);
+    DIAG_ADD(1);
     if (i != kNafLen - 1) t12_sqr_fast(T, F, S_F, S_F);
+    DIAG_ADD(2);
     apply_lines(T, F, C, has_fixed);
+    DIAG_ADD(3);
     int d = naf[i - 1];
     if (d != 0) {
       load_fixed_line(T, F, tab, s++);
+      DIAG_ADD(0);
       if (d > 0) g2_program(T, F, kProgADD_POS);
       else g2_program(T, F, kProgADD_NEG);
+      DIAG_ADD(4);
       apply_lines(T, F, C, has_fixed);
+      DIAG_ADD(3);
     }
   }
   load_fixed_line(T, F, tab, s++);
@@ -397,10 +428,27 @@ __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const L
     C.qx = gx;
     C.qy = gy;
   }
+#ifdef HG_DIAG
+  if (threadIdx.x < 16) hg_diag_acc[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t diag_start = __builtin_amdgcn_s_memtime();
+#endif
   team_miller_check(T, F, C, tab, true);
+#ifdef HG_DIAG
+  uint64_t diag_mid = __builtin_amdgcn_s_memtime();
+#endif
   team_final_exp(T, F);
   bool ok = t12_is_one(T, S_F);
   if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
+#ifdef HG_DIAG
+  uint64_t diag_end = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {
+    for (int k = 0; k < 8; k++) g_diag[blockIdx.x * 16 + k] = hg_diag_acc[k];
+    g_diag[blockIdx.x * 16 + 8] = diag_mid - diag_start;
+    g_diag[blockIdx.x * 16 + 9] = diag_end - diag_mid;
+    g_diag[blockIdx.x * 16 + 10] = diag_end - diag_start;
+  }
+#endif
 }
 
 // bn256.Pair(g1, g2).Marshal() for n pairs (GT = 1 when either is infinity)
@@ -441,6 +489,65 @@ __global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* 
     // comp 0 (x) first, comp 1 (y) second
     uint8_t* o = gt_out + (size_t)idx * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0);
     fp_to_be(o, v);
+  }
+}
+
+// Team Fp12 op probe (parity tests of the building blocks): inputs/outputs are
+// 384-byte GT-marshal-ordered canonical elements.
+//   op 0 a*b, 1 a^2 (merged products), 2 cyclotomic a^2, 3 a^p, 4 a^(p^2),
+//   5 a^-1, 6 conj(a), 7 a^u (cyclotomic), 8 final exponentiation
+__global__ __launch_bounds__(64) void k_fp12_op(int op, const uint8_t* a, const uint8_t* b, int n, uint8_t* out) {
+  __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
+  Team T = make_team(lds, kTeamWords);
+  uint32_t* F = T.base + kSlots * kFp12Words;
+  int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
+  bool valid = idx < n;
+  int ci = valid ? idx : n - 1;
+  const int pos[6] = {5, 2, 4, 1, 3, 0};
+  if (T.active) {
+    Fp v;
+    bool ge;
+    fp_from_be(v, a + (size_t)ci * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0), &ge);
+    st_fp(slot(T, S_A) + T.e * 10, v);
+    fp_from_be(v, b + (size_t)ci * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0), &ge);
+    st_fp(slot(T, S_B) + T.e * 10, v);
+  }
+  team_sync();
+  {
+    Fp z, one;
+    fp_zero(z);
+    fp_one(one);
+    if (T.tl == 0) {
+      st_fp(F + R_ZERO * 10, z);
+      st_fp(F + R_ONE * 10, one);
+    }
+    team_sync();
+  }
+  // op bits 8..: repetitions (timing of one building block: reps - 1 extra
+  // applications feed the result back as the input)
+  int reps = (op >> 8) > 0 ? (op >> 8) : 1;
+  op &= 255;
+  for (int r = 0; r < reps; r++) {
+    if (r > 0) t12_copy(T, S_A, S_F);
+    switch (op) {  // kernel-uniform
+      case 0: t12_mul(T, S_F, S_A, S_B); break;
+      case 1: t12_sqr_fast(T, S_F, S_A); break;
+      case 2: t12_cyc_sqr(T, S_F, S_A); break;
+      case 3: t12_frob(T, S_F, S_A); break;
+      case 4: t12_frob2(T, S_F, S_A); break;
+      case 5: t12_inv(T, S_F, S_A, S_K, S_L); break;
+      case 6: t12_conj(T, S_F, S_A); break;
+      case 7: t12_pow_u_cyc(T, F, S_F, S_A); break;
+      case 8: t12_copy(T, S_F, S_A); team_final_exp(T, F); break;
+      case 9: t12_sqr_table(T, F, S_F, S_A); break;
+      case 10: t12_cyc_sqr_table(T, F, S_F, S_A); break;
+      default: t12_copy(T, S_F, S_A); break;
+    }
+  }
+  if (valid && T.active) {
+    Fp v;
+    ld_fp(v, slot(T, S_F) + T.e * 10);
+    fp_to_be(out + (size_t)idx * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0), v);
   }
 }
 
@@ -527,6 +634,26 @@ __global__ void k_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t*
   g1_affine(x, y, r);
   fp_to_be(o, x);
   fp_to_be(o + 32, y);
+}
+
+// batched PublicKey.Combine (bn256/go/bn256.go:97-105): out[i] = a[i] + b[i] (G2)
+__global__ void k_g2_combine(const PointG2* a, const PointG2* b, int n, PointG2* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2J pa, pb, r;
+  if (a[i].inf) g2_set_inf(pa); else { pa.x = a[i].x; pa.y = a[i].y; f2_one(pa.z); }
+  if (b[i].inf) g2_set_inf(pb); else { pb.x = b[i].x; pb.y = b[i].y; f2_one(pb.z); }
+  g2_add(r, pa, pb);
+  PointG2 P;
+  if (g2_is_inf(r)) {
+    f2_zero(P.x);
+    f2_zero(P.y);
+    P.inf = 1;
+  } else {
+    g2_affine(P.x, P.y, r);
+    P.inf = 0;
+  }
+  out[i] = P;
 }
 
 // ------------------------------------------------------------------ copy helpers
@@ -618,6 +745,22 @@ void launch_sig_into_checks(const PointG1* sigs, int n, CheckIn* out, hipStream_
 }
 void launch_extract_pk(const CheckIn* in, int n, PointG2* out, hipStream_t s) {
   if (n > 0) k_extract_pk<<<nblk(n, 64), 64, 0, s>>>(in, n, out);
+}
+void launch_g2_combine(const PointG2* a, const PointG2* b, int n, PointG2* out, hipStream_t s) {
+  if (n > 0) k_g2_combine<<<nblk(n, 64), 64, 0, s>>>(a, b, n, out);
+}
+void launch_fp12_op(int op, const uint8_t* a, const uint8_t* b, int n, uint8_t* out, hipStream_t s) {
+  if (n > 0) k_fp12_op<<<nblk(n, kTeamsPerBlock), 64, 0, s>>>(op, a, b, n, out);
+}
+int diag_read(uint64_t* out, size_t n) {
+#ifdef HG_DIAG
+  if (n > 4096 * 16) n = 4096 * 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+#else
+  (void)out;
+  (void)n;
+  return -1;
+#endif
 }
 void launch_fp_mul(const uint32_t* a, const uint32_t* b, int n, uint32_t* out, hipStream_t s) {
   if (n > 0) k_fp_mul<<<nblk(n, 64), 64, 0, s>>>(a, b, n, out);

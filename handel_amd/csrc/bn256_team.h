@@ -57,7 +57,24 @@ HG_DEV Team make_team(uint32_t* lds_base, int words_per_team) {
   return T;
 }
 
-// r = T/R mod p for T < 64 p^2 (REDC output < 5p): two conditional subtractions
+// Reduce a normalized-limb value < 8p (limb 9 holds the top bits) to [0, p):
+// q = floor(top / (p9 + 1)) underestimates floor(value / p) by at most one,
+// so one conditional subtraction finishes.
+HG_DEV void fp_reduce8(Fp& r, const uint32_t* x) {
+  constexpr uint32_t p9 = p_top_limb();
+  uint32_t q = x[9] / (p9 + 1u);
+  uint32_t y[10];
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    int32_t v = (int32_t)x[i] - (int32_t)(q * p_limb(i)) + c;
+    y[i] = (i < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
+    c = v >> 26;
+  }
+  fp_csub(r, y);
+}
+
+// Montgomery REDC for T < ~199 p^2 (output < 8p), then full reduction.
 HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -74,19 +91,7 @@ HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
     x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
     carry = v >> 26;
   }
-  // subtract 2p if x >= 2p, then p if x >= p
-  const uint32_t p2[10] = {HG_2PLIMBS};
-  uint32_t s[10];
-  int32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    int32_t d = (int32_t)x[i] - (int32_t)p2[i] - br;
-    br = (d >> 31) & 1;
-    s[i] = (uint32_t)d & kMask;
-  }
-#pragma unroll
-  for (int i = 0; i < 10; i++) x[i] = br ? x[i] : s[i];
-  fp_csub(r, x);
+  fp_reduce8(r, x);
 }
 
 // conditional pieces used by the coefficient kernels
@@ -149,6 +154,126 @@ HG_DEV void t12_mul(const Team& T, int dst, int sa, int sb) {
 }
 
 HG_DEV void t12_sqr(const Team& T, int dst, int sa) { t12_mul(T, dst, sa, sa); }
+
+// acc += v * R (R = 2^260 = 2^(26*10)): adds the Montgomery-form value v to
+// the product sum, i.e. a linear term costs 10 adds instead of a product.
+HG_DEV void acc_add_shifted(Acc& acc, const Fp& v) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) acc.c[10 + i] += v.l[i];
+}
+
+// small constant multiple of a loose element, limb-wise (no carries)
+template <int K>
+HG_DEV void fp_scale(Fp& r, const Fp& a) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.l[i] = a.l[i] * K;
+}
+
+// dst = a^2 with the symmetric products merged: lane (k, c) sums 4 terms
+// (i, j, mult, wrap) over pairs i <= j, i + j = k (mod 6), 8 products.
+HG_DEV void t12_sqr_fast(const Team& T, int dst, int sa) {
+  const uint32_t* A = slot(T, sa);
+  // per-k term tables packed 4 bits per k (k = 0..5): i, j, multiplier, wrap flag
+  //   k:      0        1        2        3        4        5
+  //   t=0  (1,5,2,w) (0,1,2)  (0,2,2)  (0,3,2)  (0,4,2)  (0,5,2)
+  //   t=1  (2,4,2,w) (2,5,2,w)(3,5,2,w)(1,2,2)  (1,3,2)  (1,4,2)
+  //   t=2  (0,0,1)   (3,4,2,w)(1,1,1)  (4,5,2,w)(2,2,1)  (2,3,2)
+  //   t=3  (3,3,1,w)  -       (4,4,1,w) -       (5,5,1,w) -
+  const uint32_t I[4] = {0x000001u, 0x111322u, 0x224130u, 0x050403u};
+  const uint32_t J[4] = {0x543215u, 0x432554u, 0x325140u, 0x050403u};
+  const uint32_t M[4] = {0x222222u, 0x222222u, 0x212121u, 0x010101u};  // 0 = dummy term
+  const uint32_t W[4] = {0x000001u, 0x000111u, 0x001010u, 0x010101u};
+  const int sh = 4 * T.k;
+  Acc acc;
+  acc_zero(acc);
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    int i = (I[t] >> sh) & 15, j = (J[t] >> sh) & 15;
+    uint32_t m = (M[t] >> sh) & 15;
+    bool wrap = ((W[t] >> sh) & 15) != 0;
+    Fp2 X, Y;
+    ld_f2(X, A, i);
+    ld_f2(Y, A, j);
+    // the multiplier goes on Y: term_operands negates X, which needs X < p
+#pragma unroll
+    for (int l = 0; l < 10; l++) {
+      Y.x.l[l] *= m;
+      Y.y.l[l] *= m;
+    }
+    Fp u1, u2;
+    term_operands(u1, u2, X, wrap, T.comp);
+    acc_mad(acc, u1, Y.y);
+    acc_mad(acc, u2, Y.x);
+  }
+  Fp r;
+  acc_reduce_wide(r, acc);
+  team_sync();
+  if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
+  team_sync();
+}
+
+// Granger-Scott squaring in the cyclotomic subgroup (valid after the easy part
+// of the final exponentiation). With f = (c0 + c3 s) + (c1 + c4 s) w + (c2 + c5 s) w^2,
+// s = w^3, each group (a, b) squares in Fp4: (a^2 + xi b^2) + 2ab s, and
+//   c0' = 3(a^2 + xi b^2) - 2c0   c3' = 6ab + 2c3      for (a, b) = (c0, c3)
+//   c2' = 3(a^2 + xi b^2) - 2c2   c5' = 6ab + 2c5      for (a, b) = (c1, c4)
+//   c4' = 3(a^2 + xi b^2) - 2c4   c1' = 6 xi ab + 2c1  for (a, b) = (c2, c5)
+// Each lane: 3 products; the +-2c term is added to the high columns.
+HG_DEV void t12_cyc_sqr(const Team& T, int dst, int sa) {
+  const uint32_t* A = slot(T, sa);
+  const int k = T.k;
+  const int ga = (k == 0 || k == 3) ? 0 : ((k == 2 || k == 5) ? 1 : 2);
+  const bool sq = (k & 1) == 0;   // k = 0, 2, 4: the a^2 + xi b^2 lanes
+  const bool xi = (k == 1);       // the 6 xi ab lane
+  const bool cx = T.comp == 0;
+  Fp2 a, b;
+  ld_f2(a, A, ga);
+  ld_f2(b, A, ga + 3);
+  Fp c;
+  ld_fp(c, A + T.e * 10);
+  Fp nax, nay, nbx, da, db, sa_, sb_;
+  fp_neg_loose(nax, a.x);
+  fp_neg_loose(nay, a.y);
+  fp_neg_loose(nbx, b.x);
+  fp_sub(da, a.y, a.x);
+  fp_sub(db, b.y, b.x);
+  fp_add_loose(sa_, a.y, a.x);
+  fp_add_loose(sb_, b.y, b.x);
+  Fp u1, v1, u2, v2, u3;
+#pragma unroll
+  for (int l = 0; l < 10; l++) {
+    // sq lanes: x: (6ax)ay + (18bx)by + (3sb)db ; y: (3sa)da + (6nbx)by + (9sb)db
+    // ab lanes: x: (6ax)by + (6ay)bx ; y: (6ay)by + (6nax)bx
+    // xi lane:  x: 6(3ax+ay)by + 6(3ay+nax)bx ; y: 6(3ay+nax)by + 6(3nax+nay)bx
+    uint32_t xa = 3 * a.x.l[l] + a.y.l[l], xb = 3 * a.y.l[l] + nax.l[l], xc = 3 * nax.l[l] + nay.l[l];
+    uint32_t sq_u1 = cx ? 6 * a.x.l[l] : 3 * sa_.l[l];
+    uint32_t sq_v1 = cx ? a.y.l[l] : da.l[l];
+    uint32_t sq_u2 = cx ? 18 * b.x.l[l] : 6 * nbx.l[l];
+    uint32_t ab_u1 = xi ? 6 * (cx ? xa : xb) : 6 * (cx ? a.x.l[l] : a.y.l[l]);
+    uint32_t ab_u2 = xi ? 6 * (cx ? xb : xc) : 6 * (cx ? a.y.l[l] : nax.l[l]);
+    u1.l[l] = sq ? sq_u1 : ab_u1;
+    v1.l[l] = sq ? sq_v1 : b.y.l[l];
+    u2.l[l] = sq ? sq_u2 : ab_u2;
+    v2.l[l] = sq ? b.y.l[l] : b.x.l[l];
+    u3.l[l] = sq ? (cx ? 3 * sb_.l[l] : 9 * sb_.l[l]) : 0u;
+  }
+  Acc acc;
+  acc_zero(acc);
+  acc_mad(acc, u1, v1);
+  acc_mad(acc, u2, v2);
+  acc_mad(acc, u3, db);
+  // linear term: -2c on the a^2 lanes, +2c on the others (added as 2c R or 2(p - c) R)
+  Fp nc, lin;
+  fp_neg_loose(nc, c);
+  fp_sel(lin, sq, nc, c);
+  fp_scale<2>(lin, lin);
+  acc_add_shifted(acc, lin);
+  Fp r;
+  acc_reduce_wide(r, acc);
+  team_sync();
+  if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
+  team_sync();
+}
 
 // dst = a * (c + b w + a3 w^3) for line coefficients held in registers
 HG_DEV void t12_mul_line(const Team& T, int dst, int sa, const Fp2& la, const Fp2& lb, const Fp2& lc) {

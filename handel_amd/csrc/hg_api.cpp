@@ -516,6 +516,32 @@ int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   return HG_OK;
 }
 
+int hg_combine_g2(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out, int32_t* codes) {
+  if (!c || (n && (!a || !b || !out || !codes))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 128 * 2));
+  HG_CHECK(c, c->pts2.ensure(n * 3));
+  HG_CHECK(c, c->codes_a.ensure(n));
+  HG_CHECK(c, c->codes_b.ensure(n));
+  HG_CHECK(c, c->codes_c.ensure(n));
+  uint8_t* d = c->bytes_a.p;
+  HG_CHECK(c, hipMemcpyAsync(d, a, n * 128, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(d + n * 128, b, n * 128, hipMemcpyHostToDevice, c->stream));
+  launch_decode_g2(d, (int)n, c->flavor, c->pts2.p, c->codes_a.p, c->stream);
+  launch_decode_g2(d + n * 128, (int)n, c->flavor, c->pts2.p + n, c->codes_b.p, c->stream);
+  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, c->codes_c.p, c->stream);
+  launch_g2_combine(c->pts2.p, c->pts2.p + n, (int)n, c->pts2.p + 2 * n, c->stream);
+  launch_encode_g2(c->pts2.p + 2 * n, (int)n, d, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(out, d, n * 128, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
 int hg_pair(hg_ctx* c, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t* gt_out, int32_t* codes) {
   if (!c || (n && (!g1s || !g2s || !gt_out || !codes))) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
@@ -581,6 +607,31 @@ int hg_sign(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out) {
   HG_CHECK(c, hipMemcpyAsync(sigs_out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
+}
+
+int hg_debug_fp12(hg_ctx* c, int op, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out) {
+  if (!c || (n && (!a || !b || !out))) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 384 * 3));
+  uint8_t* d = c->bytes_a.p;
+  HG_CHECK(c, hipMemcpyAsync(d, a, n * 384, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(d + n * 384, b, n * 384, hipMemcpyHostToDevice, c->stream));
+  launch_fp12_op(op, d, d + n * 384, (int)n, d + 2 * n * 384, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(out, d + 2 * n * 384, n * 384, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_diag_read(hg_ctx* c, uint64_t* out, size_t n) {
+  if (!c || !out) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return diag_read(out, n) == 0 ? HG_OK : HG_ERR_ARG;
 }
 
 int hg_timing_enable(hg_ctx* c, int on) {

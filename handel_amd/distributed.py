@@ -1,0 +1,50 @@
+"""Multi-GPU sharding of independent verification batches.
+
+One process per GPU. Checks are independent, so the batch is split into
+contiguous slices (or, for N committees, one committee per GPU) with the
+registry and H(m) replicated; the only exchange is a gather of the per-rank
+verdict bitsets (bit i = check i valid, willf layout: byte j holds checks
+8j..8j+7, LSB first) over RCCL (backend "nccl") — or gloo on CPU tests.
+"""
+
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import torch
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous slice [lo, hi) of n checks for `rank` (sizes differ by <= 1)."""
+    lo = n * rank // world
+    hi = n * (rank + 1) // world
+    return lo, hi
+
+
+def pack_verdicts(codes: torch.Tensor) -> torch.Tensor:
+    """int32 verdict codes -> uint8 bitset of valid checks (code == 0)."""
+    n = codes.numel()
+    nbits = (n + 7) // 8 * 8
+    ok = torch.zeros(nbits, dtype=torch.int32, device=codes.device)
+    ok[:n] = (codes == 0).to(torch.int32)
+    weights = (2 ** torch.arange(8, device=codes.device, dtype=torch.int32)).view(1, 8)
+    return (ok.view(-1, 8) * weights).sum(dim=1).to(torch.uint8)
+
+
+def unpack_verdicts(bits: torch.Tensor, n: int) -> torch.Tensor:
+    b = bits.to(torch.int32).view(-1, 1)
+    shifts = torch.arange(8, device=bits.device, dtype=torch.int32).view(1, 8)
+    return ((b >> shifts) & 1).view(-1)[:n].to(torch.bool)
+
+
+def gather_verdicts(bits: torch.Tensor, world: int, out: List[torch.Tensor] = None) -> List[torch.Tensor]:
+    """all_gather of equal-size bitsets (every rank gets every rank's verdicts)."""
+    import torch.distributed as dist
+
+    if out is None:
+        out = [torch.empty_like(bits) for _ in range(world)]
+    if world == 1:
+        out[0].copy_(bits)
+        return out
+    dist.all_gather(out, bits)
+    return out

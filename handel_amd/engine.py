@@ -136,6 +136,14 @@ class Engine:
         self._check(self.L.hg_combine_g1(self.ctx, _ptr(x), _ptr(y), n, _ptr(out), _ptr(codes)), "hg_combine_g1")
         return out.tobytes(), codes
 
+    def combine_g2(self, a: bytes, b: bytes) -> Tuple[bytes, np.ndarray]:
+        x, y = _u8(a), _u8(b)
+        n = len(x) // 128
+        out = np.zeros(n * 128, dtype=np.uint8)
+        codes = np.zeros(n, dtype=np.int32)
+        self._check(self.L.hg_combine_g2(self.ctx, _ptr(x), _ptr(y), n, _ptr(out), _ptr(codes)), "hg_combine_g2")
+        return out.tobytes(), codes
+
     def pair(self, g1s: bytes, g2s: bytes) -> Tuple[bytes, np.ndarray]:
         x, y = _u8(g1s), _u8(g2s)
         n = len(x) // 64
@@ -156,6 +164,15 @@ class Engine:
         n = len(s) // 32
         out = np.zeros(n * 64, dtype=np.uint8)
         self._check(self.L.hg_sign(self.ctx, _ptr(s), n, _ptr(out)), "hg_sign")
+        return out.tobytes()
+
+    def fp12_op(self, op: int, a: bytes, b: bytes = None) -> bytes:
+        """Team Fp12 building-block probe (hg_debug_fp12); 384-byte GT marshals."""
+        x = _u8(a)
+        y = _u8(b) if b is not None else x
+        n = len(x) // 384
+        out = np.zeros(n * 384, dtype=np.uint8)
+        self._check(self.L.hg_debug_fp12(self.ctx, op, _ptr(x), _ptr(y), n, _ptr(out)), "hg_debug_fp12")
         return out.tobytes()
 
     def fp_mul(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:

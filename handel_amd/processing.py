@@ -1,0 +1,90 @@
+"""Batched replacement of Handel's evaluator verification.
+
+processing.go's evaluatorProcessing verifies ONE incoming multisignature per
+loop iteration (readTodos picks the best, verifyAndPublish checks it,
+processing.go:171-287). `BatchVerifier` takes the same requests — a level,
+its bitset and the aggregate signature — and verifies many per GPU launch:
+the registry lives on the GPU, H(m) is computed once, and every request is a
+(level range, bitset) -> aggregate key -> pairing check. Verdicts are a pure
+function of (msg, range, bitset, sig), so batching cannot change them.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import partitioner as part
+from ._lib import HG_OK
+from .engine import REQ_DTYPE, Engine
+
+
+@dataclass
+class IncomingSig:
+    """processing.go:61-66 incomingSig: origin, level, multisig."""
+    origin: int
+    level: int
+    bits: Sequence[bool]
+    sig: bytes
+
+
+class BatchVerifier:
+    def __init__(self, eng: Engine, registry_pks: bytes, msg: bytes, node_id: int = 0):
+        self.eng = eng
+        self.n = len(registry_pks) // 128
+        codes = eng.registry_load(registry_pks)
+        if codes.any():
+            raise ValueError(f"registry key {int(np.flatnonzero(codes)[0])} fails to unmarshal")
+        self.hash_rc = eng.set_message(msg)
+        self.node_id = node_id
+
+    def _pack(self, items):
+        reqs = np.zeros(len(items), dtype=REQ_DTYPE)
+        words: List[np.ndarray] = []
+        nw = 0
+        sigs = bytearray()
+        for i, (lo, size, bits, sig) in enumerate(items):
+            w = part.bits_to_words(bits)
+            reqs[i] = (lo, len(bits), size, nw)
+            words.append(w)
+            nw += len(w)
+            s = bytes(sig)
+            sigs += s[:64].ljust(64, b"\x00") if len(s) != 64 else s
+        allw = np.concatenate(words) if words else np.zeros(0, dtype=np.uint64)
+        return reqs, allw, bytes(sigs)
+
+    def verify_levels(self, sigs: Sequence[IncomingSig]) -> List[Optional[str]]:
+        """verifySignature (processing.go:342-368) for each incoming sig, as
+        seen by node `node_id`; returns None or the reference's error text."""
+        items, errs = [], []
+        for s in sigs:
+            try:
+                lo, hi = part.range_level(self.node_id, self.n, s.level)
+                items.append((lo, hi - lo, s.bits, s.sig))
+                errs.append(None)
+            except part.PartitionerError as e:
+                items.append((0, 0, [], bytes(64)))
+                errs.append(str(e))
+        codes = self.eng.verify_aggregate(*self._pack(items)) if items else []
+        out = []
+        for e, c in zip(errs, codes):
+            if e is not None:
+                out.append(e)
+            elif c == HG_OK:
+                out.append(None)
+            else:
+                out.append("handel: " + self.eng.code_string(int(c)))
+        return out
+
+    def verify_ranges(self, items) -> np.ndarray:
+        """Raw codes for (offset, level_size, bits, sig) requests."""
+        return self.eng.verify_aggregate(*self._pack(items))
+
+    def verify_multisignature(self, bits: Sequence[bool], sig: bytes) -> Optional[str]:
+        """crypto.go:120-137 VerifyMultiSignature over the whole registry."""
+        if len(bits) != self.n:
+            return "verify multisignature: inconsistent sizes"
+        c = self.verify_ranges([(0, self.n, bits, sig)])[0]
+        return None if c == HG_OK else self.eng.code_string(int(c))

@@ -109,6 +109,10 @@ int hg_aggregate_pk(hg_ctx* ctx, const hg_request* reqs, size_t n, const uint64_
 /* Batched SigBLS.Combine (bn256/go/bn256.go:192-200): out[i] = a[i] + b[i]. */
 int hg_combine_g1(hg_ctx* ctx, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out, int32_t* codes);
 
+/* Batched PublicKey.Combine on marshalled keys (bn256/go/bn256.go:97-105):
+ * out[i] = a[i] + b[i] in G2 (n*128 B each). */
+int hg_combine_g2(hg_ctx* ctx, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out, int32_t* codes);
+
 /* bn256.Pair(g1[i], g2[i]).Marshal() — the GT values the reference compares
  * in VerifySignature (bn256/go/bn256.go:88-89); parity probe. */
 int hg_pair(hg_ctx* ctx, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t* gt_out, int32_t* codes);
@@ -130,6 +134,15 @@ int hg_debug_fp_mul(hg_ctx* ctx, const uint32_t* a, const uint32_t* b, size_t n,
  * returns (and clears) the summed kernel time and the number of launches. */
 int hg_timing_enable(hg_ctx* ctx, int on);
 int hg_timing_read(hg_ctx* ctx, double* total_ms, int* launches);
+
+/* Parity probe of the team Fp12 building blocks: elements are 384-byte GT
+ * marshals. op: 0 a*b, 1 a^2, 2 cyclotomic a^2, 3 a^p, 4 a^(p^2), 5 a^-1,
+ * 6 conj(a), 7 a^u, 8 final exponentiation, 9/10 table-program squarings. */
+int hg_debug_fp12(hg_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out);
+
+/* Diagnostic builds only (-DHG_DIAG, tools/diag.py): per-block s_memtime
+ * phase counters of the last pairing-check launch; HG_ERR_ARG otherwise. */
+int hg_diag_read(hg_ctx* ctx, uint64_t* out, size_t n);
 
 /* Wait for all work submitted on the context's stream. */
 int hg_sync(hg_ctx* ctx);

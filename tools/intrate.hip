@@ -53,6 +53,26 @@ __global__ __launch_bounds__(256) void k_add(uint64_t* out, uint32_t seed) {
   if (s == 0x12345) out[0] = s;
 }
 
+#define CHAIN8(INSN)                                                                           \
+  asm volatile(INSN " %0, %8, %0\n\t" INSN " %1, %8, %1\n\t" INSN " %2, %8, %2\n\t" INSN        \
+                    " %3, %8, %3\n\t" INSN " %4, %8, %4\n\t" INSN " %5, %8, %5\n\t" INSN          \
+                    " %6, %8, %6\n\t" INSN " %7, %8, %7\n\t"                                       \
+               : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7) \
+               : "v"(a))
+
+#define K32(NAME, INSN)                                                                 \
+  __global__ __launch_bounds__(256) void NAME(uint64_t* out, uint32_t seed) {           \
+    uint32_t a = seed ^ threadIdx.x, b = seed * 2654435761u + blockIdx.x;               \
+    uint32_t c0 = a, c1 = b, c2 = a + 1, c3 = b + 1, c4 = a + 2, c5 = b + 2, c6 = a + 3, \
+             c7 = b + 3;                                                                \
+    for (int it = 0; it < ITERS; it++) CHAIN8(INSN);                                    \
+    uint64_t s = c0 ^ c1 ^ c2 ^ c3 ^ c4 ^ c5 ^ c6 ^ c7;                                 \
+    if (s == 0x12345) out[0] = s;                                                       \
+  }
+K32(k_mul_lo, "v_mul_lo_u32")
+K32(k_mul_u24, "v_mul_u32_u24")
+K32(k_lshl, "v_lshlrev_b32")
+
 template <typename K>
 double run(K kern, int blocks, uint64_t* d) {
   hipEvent_t e0, e1;
@@ -80,6 +100,9 @@ int main() {
     int blocks = cus * per_cu;  // 256-thread blocks: per_cu waves per SIMD
     printf("{\"op\": \"v_mad_u64_u32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_mad, blocks, d));
     printf("{\"op\": \"v_add_u32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_add, blocks, d));
+    printf("{\"op\": \"v_mul_lo_u32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_mul_lo, blocks, d));
+    printf("{\"op\": \"v_mul_u32_u24\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_mul_u24, blocks, d));
+    printf("{\"op\": \"v_lshlrev_b32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_lshl, blocks, d));
   }
   (void)hipFree(d);
   return 0;
