@@ -79,6 +79,25 @@ def make_batch(eng: Engine, n: int, seed: int):
     return pks, bytes(sigs), expect
 
 
+def pmc_traffic():
+    """HBM bytes per k_verify launch from the newest committed PMC summary
+    (profiles/*_pmc.csv, written by tools/profile_round.sh +
+    tools/rocpd_summary.py): FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE."""
+    import csv
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.csv")), key=os.path.getmtime)
+    for path in reversed(files):
+        vals = {}
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["kernel"] == "hg::k_verify":
+                    vals[row["counter"]] = float(row["avg"])
+        if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+            return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(n_sample: int, pks: bytes, sigs: bytes, expect: np.ndarray):
     """The reference algorithm restated in C (oracle/bn256_ref.c, 'port'):
     two full pairings + GT compare per check, timed on this host's cores."""
@@ -162,8 +181,10 @@ def main():
     value = total / dt
     avg_kernel_ms = kern_ms / max(launches, 1)
     achieved = n * FPMUL_PER_CHECK * MADS_PER_FPMUL / (avg_kernel_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic()
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": P_MAD_TOPS, "unit": "Tmad/s",
-                "frac": round(achieved / P_MAD_TOPS, 4), "traffic": None,
+                "frac": round(achieved / P_MAD_TOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": traffic_src,
                 "kernel": "k_verify", "kernel_ms": round(avg_kernel_ms, 4),
                 "work_per_check": f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads"}
     cpu = None
