@@ -4,37 +4,19 @@
 //                               (x/crypto / cloudflare Unmarshal rules, a9)
 //   k_hash_point                k * G1 for the hashedMessage scalar (a7)
 //   k_g2_lines                  the fixed G2Base line table (precomputed once)
-//   k_verify                    product-of-pairings check, one 16-lane team
-//                               per check: e(H, pk) * e(-sig, G2Base) == 1 (a6)
-//   k_pair                      bn256.Pair(g1, g2) -> GT marshal (parity probe)
+//   (k_verify: bn256_verify.hip; k_pair and the Fp12 probe: bn256_pair.hip)
 //   k_aggregate                 bitset-driven G2 Combine fold, one wave per
 //                               request, LDS tree reduction (a3, a4, a5)
 //   k_g1_combine                batched SigBLS.Combine (a8)
 //   k_fp_mul                    field self-test
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include "bn256_kernels.h"
-#include "bn256_g2team.h"
+#include "bn256_curve.h"
 
 namespace hg {
 
-// ------------------------------------------------------------------ diagnostics
-// Built only with -DHG_DIAG (tools/diag.py builds a separate library): lane 0
-// of every block accumulates s_memtime cycles per phase of k_verify.
-#ifdef HG_DIAG
-__shared__ uint64_t hg_diag_acc[16];
-__device__ uint64_t g_diag[4096 * 16];
-#define DIAG_T0() uint64_t diag_t0_ = __builtin_amdgcn_s_memtime()
-#define DIAG_ADD(k)                                                     \
-  do {                                                                  \
-    uint64_t diag_t1_ = __builtin_amdgcn_s_memtime();                   \
-    if (threadIdx.x == 0) hg_diag_acc[k] += diag_t1_ - diag_t0_;        \
-    diag_t0_ = diag_t1_;                                                \
-  } while (0)
-#else
-#define DIAG_T0() (void)0
-#define DIAG_ADD(k) (void)0
-#endif
 
 // ------------------------------------------------------------------ decode
 // Unmarshal rules:
@@ -238,319 +220,6 @@ __global__ void k_g2_lines(LineCoef* tab) {
   line_add(tab[s].a, tab[s].bx, tab[s].cy, R, q2x, qy, r2);
 }
 
-// ------------------------------------------------------------------ team Miller loop + final exp
-// LDS layout per team: 12 Fp12 slots followed by the per-check constants.
-enum { S_F = 0, S_A, S_B, S_C, S_D, S_E, S_G, S_H, S_I, S_J, S_K, S_L, kSlots };
-static constexpr int kTeamWords = kSlots * kFp12Words + kG2Regs * 10;
-static constexpr int kTeamsPerBlock = 4;
-
-// the pairing's final exponentiation (x/crypto optate.go finalExponentiation)
-HG_DEV void team_final_exp(const Team& T, uint32_t* F) {
-  DIAG_T0();
-  t12_inv(T, S_A, S_F, S_K, S_L);  // A = f^-1
-  DIAG_ADD(5);
-  t12_conj(T, S_B, S_F);           // B = conj(f)
-  t12_mul(T, S_F, S_B, S_A);       // t1 = f^(p^6 - 1)
-  t12_frob2(T, S_A, S_F);
-  t12_mul(T, S_F, S_F, S_A);       // t1 = t1^(p^2 + 1)
-  t12_frob(T, S_A, S_F);           // fp
-  t12_frob2(T, S_B, S_F);          // fp2
-  t12_mul(T, S_A, S_A, S_B);
-  t12_frob(T, S_B, S_B);           // fp3
-  t12_mul(T, S_A, S_A, S_B);       // y0 = fp * fp2 * fp3
-  DIAG_ADD(6);
-  t12_pow_u_cyc(T, F, S_C, S_F);          // fu
-  t12_pow_u_cyc(T, F, S_D, S_C);          // fu2
-  t12_pow_u_cyc(T, F, S_E, S_D);          // fu3
-  DIAG_ADD(7);
-  t12_frob(T, S_G, S_C);
-  t12_conj(T, S_G, S_G);           // y3 = conj(frob(fu))
-  t12_frob(T, S_H, S_D);
-  t12_mul(T, S_H, S_C, S_H);
-  t12_conj(T, S_H, S_H);           // y4 = conj(fu * frob(fu2))
-  t12_frob2(T, S_C, S_D);          // y2 = frob2(fu2)
-  t12_conj(T, S_D, S_D);           // y5 = conj(fu2)
-  t12_frob(T, S_I, S_E);
-  t12_mul(T, S_I, S_E, S_I);
-  t12_conj(T, S_I, S_I);           // y6 = conj(fu3 * frob(fu3))
-  t12_cyc_sqr(T, F, S_K, S_I);
-  t12_mul(T, S_K, S_K, S_H);
-  t12_mul(T, S_K, S_K, S_D);       // t0 = y6^2 y4 y5
-  t12_mul(T, S_J, S_G, S_D);
-  t12_mul(T, S_J, S_J, S_K);       // t1 = y3 y5 t0
-  t12_mul(T, S_K, S_K, S_C);       // t0 = t0 y2
-  t12_cyc_sqr(T, F, S_J, S_J);
-  t12_mul(T, S_J, S_J, S_K);
-  t12_cyc_sqr(T, F, S_J, S_J);            // t1 = (t1^2 t0)^2
-  t12_conj(T, S_L, S_F);           // y1 = conj(t1_easy)
-  t12_mul(T, S_K, S_J, S_L);       // t0 = t1 y1
-  t12_mul(T, S_J, S_J, S_A);       // t1 = t1 y0
-  t12_cyc_sqr(T, F, S_K, S_K);
-  t12_mul(T, S_F, S_K, S_J);       // result
-  DIAG_ADD(6);
-}
-
-// Per-check inputs of the team Miller loop.
-struct CheckCtx {
-  Fp2 qx, qy;   // affine pk (a dummy valid point when the pk is infinity)
-  Fp hx, hy;    // H (affine)
-  Fp sx, sy;    // sig (affine)
-  bool use_q;   // pk contributes (not infinity)
-  bool use_s;   // sig contributes (not infinity)
-};
-
-// Writes the team's G2 register file: point R = (Q, 1, 1), Q, -Qy, Qy^2, the
-// Frobenius images q1 = pi(Q), -q2 = (Qx gamma2[2], Qy) (optate.go miller),
-// the G1 points and constants.
-HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
-  const Fp2 g1[6] = HG_GAMMA1;
-  const Fp g2[6] = HG_GAMMA2;
-  Fp2 nqy, r2, q1x, q1y, q1r2, q2x, t, one2, zero2;
-  f2_neg(nqy, C.qy);
-  f2_sqr(r2, C.qy);
-  f2_conj(t, C.qx);
-  f2_mul(q1x, t, g1[2]);
-  f2_conj(t, C.qy);
-  f2_mul(q1y, t, g1[3]);
-  f2_sqr(q1r2, q1y);
-  f2_muls(q2x, C.qx, g2[2]);
-  f2_one(one2);
-  f2_zero(zero2);
-  Fp zero, one, nsy;
-  fp_zero(zero);
-  fp_one(one);
-  fp_neg(nsy, C.sy);
-  if (T.tl == 0) {
-    auto put2 = [&](int rx, const Fp2& v) {
-      st_fp(F + rx * 10, v.x);
-      st_fp(F + (rx + 1) * 10, v.y);
-    };
-    st_fp(F + R_ZERO * 10, zero);
-    st_fp(F + R_ONE * 10, one);
-    st_fp(F + R_PX * 10, C.hx);
-    st_fp(F + R_PY * 10, C.hy);
-    st_fp(F + R_SX * 10, C.sx);
-    st_fp(F + R_NSY * 10, nsy);
-    put2(R_X_x, C.qx);
-    put2(R_Y_x, C.qy);
-    put2(R_Z_x, one2);
-    put2(R_T_x, one2);
-    put2(R_QX_x, C.qx);
-    put2(R_QY_x, C.qy);
-    put2(R_NQY_x, nqy);
-    put2(R_R2_x, r2);
-    put2(R_P1X_x, q1x);
-    put2(R_P1Y_x, q1y);
-    put2(R_P1R2_x, q1r2);
-    put2(R_P2X_x, q2x);
-    put2(R_F2ONE_x, one2);
-    put2(R_F2ZERO_x, zero2);
-  }
-  team_sync();
-}
-
-// Loads the G2Base line s (a, bx, cy: 6 Fp) into FA, FBX, FCY.
-HG_DEV void load_fixed_line(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
-  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
-  if (T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
-  team_sync();
-}
-
-// f *= pk line (LA, LB, LC) and, when has_fixed, the G2Base line (FA, FB, FC).
-// A point at infinity contributes the unit line (a = b = 0, c = 1); the choice
-// is an address select, so teams of one wave stay convergent.
-HG_DEV void apply_lines(const Team& T, const uint32_t* F, const CheckCtx& C, bool has_fixed) {
-  t12_mul_line_regs(T, S_F, S_F, F, C.use_q ? R_LA_x : R_F2ZERO_x, C.use_q ? R_LB_x : R_F2ZERO_x,
-                    C.use_q ? R_LC_x : R_F2ONE_x);
-  if (has_fixed)
-    t12_mul_line_regs(T, S_F, S_F, F, C.use_s ? R_FA_x : R_F2ZERO_x, C.use_s ? R_FB_x : R_F2ZERO_x,
-                      C.use_s ? R_FC_x : R_F2ONE_x);
-}
-
-// f = Miller(pk at H) * Miller(G2Base at -sig) (x/crypto optate.go miller, with
-// the two loops sharing their squarings); the G2 steps run as team programs.
-HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, const LineCoef* tab, bool has_fixed) {
-  const int8_t naf[kNafLen] = HG_NAF;
-  t12_set_one(T, S_F);
-  g2_regs_init(T, F, C);
-  int s = 0;
-  DIAG_T0();
-  for (int i = kNafLen - 1; i > 0; i--) {
-    load_fixed_line(T, F, tab, s++);
-    DIAG_ADD(0);
-    g2_program(T, F, kProgDBL);
-    DIAG_ADD(1);
-    if (i != kNafLen - 1) t12_sqr_fast(T, F, S_F, S_F);
-    DIAG_ADD(2);
-    apply_lines(T, F, C, has_fixed);
-    DIAG_ADD(3);
-    int d = naf[i - 1];
-    if (d != 0) {
-      load_fixed_line(T, F, tab, s++);
-      DIAG_ADD(0);
-      if (d > 0) g2_program(T, F, kProgADD_POS);
-      else g2_program(T, F, kProgADD_NEG);
-      DIAG_ADD(4);
-      apply_lines(T, F, C, has_fixed);
-      DIAG_ADD(3);
-    }
-  }
-  load_fixed_line(T, F, tab, s++);
-  g2_program(T, F, kProgADD_F1);
-  apply_lines(T, F, C, has_fixed);
-  load_fixed_line(T, F, tab, s++);
-  g2_program(T, F, kProgADD_F2);
-  apply_lines(T, F, C, has_fixed);
-}
-
-HG_DEV uint32_t* team_regs(const Team& T) { return T.base + kSlots * kFp12Words; }
-
-__global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const LineCoef* tab,
-                                               const PointG1* hpt, int32_t* codes) {
-  __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
-  Team T = make_team(lds, kTeamWords);
-  uint32_t* F = team_regs(T);
-  int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
-  bool valid = idx < n;
-  int ci = valid ? idx : n - 1;
-  const CheckIn& I = in[ci];
-  CheckCtx C;
-  C.qx = I.pk.x;
-  C.qy = I.pk.y;
-  C.hx = hpt->x;
-  C.hy = hpt->y;
-  C.sx = I.sig.x;
-  C.sy = I.sig.y;
-  C.use_q = I.pk.inf == 0;
-  C.use_s = I.sig.inf == 0;
-  if (!C.use_q) {  // keep the (unused) doubling chain well-defined
-    const Fp2 gx = HG_G2X, gy = HG_G2Y;
-    C.qx = gx;
-    C.qy = gy;
-  }
-#ifdef HG_DIAG
-  if (threadIdx.x < 16) hg_diag_acc[threadIdx.x] = 0;
-  __syncthreads();
-  uint64_t diag_start = __builtin_amdgcn_s_memtime();
-#endif
-  team_miller_check(T, F, C, tab, true);
-#ifdef HG_DIAG
-  uint64_t diag_mid = __builtin_amdgcn_s_memtime();
-#endif
-  team_final_exp(T, F);
-  bool ok = t12_is_one(T, S_F);
-  if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
-#ifdef HG_DIAG
-  uint64_t diag_end = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {
-    for (int k = 0; k < 8; k++) g_diag[blockIdx.x * 16 + k] = hg_diag_acc[k];
-    g_diag[blockIdx.x * 16 + 8] = diag_mid - diag_start;
-    g_diag[blockIdx.x * 16 + 9] = diag_end - diag_mid;
-    g_diag[blockIdx.x * 16 + 10] = diag_end - diag_start;
-  }
-#endif
-}
-
-// bn256.Pair(g1, g2).Marshal() for n pairs (GT = 1 when either is infinity)
-__global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* g2s, int n, const LineCoef* tab,
-                                             uint8_t* gt_out) {
-  __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
-  Team T = make_team(lds, kTeamWords);
-  uint32_t* F = team_regs(T);
-  int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
-  bool valid = idx < n;
-  int ci = valid ? idx : n - 1;
-  PointG1 P = g1s[ci];
-  PointG2 Q = g2s[ci];
-  CheckCtx C;
-  C.use_q = (P.inf == 0) && (Q.inf == 0);
-  C.use_s = false;
-  if (!C.use_q) {
-    const Fp2 gx = HG_G2X, gy = HG_G2Y;
-    Q.x = gx;
-    Q.y = gy;
-    const Fp hx = HG_G1X, hy = HG_G1Y;
-    P.x = hx;
-    P.y = hy;
-  }
-  C.qx = Q.x;
-  C.qy = Q.y;
-  C.hx = P.x;
-  C.hy = P.y;
-  fp_zero(C.sx);
-  fp_zero(C.sy);
-  team_miller_check(T, F, C, tab, false);
-  team_final_exp(T, F);  // f == 1 when either input is infinity, and 1^e == 1
-  // GT.Marshal order: coefficients 5,3,1,4,2,0, each as (x, y)
-  if (valid && T.active) {
-    const int pos[6] = {5, 2, 4, 1, 3, 0};  // position of coefficient k in the marshal
-    Fp v;
-    ld_fp(v, slot(T, S_F) + T.e * 10);
-    // comp 0 (x) first, comp 1 (y) second
-    uint8_t* o = gt_out + (size_t)idx * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0);
-    fp_to_be(o, v);
-  }
-}
-
-// Team Fp12 op probe (parity tests of the building blocks): inputs/outputs are
-// 384-byte GT-marshal-ordered canonical elements.
-//   op 0 a*b, 1 a^2 (merged products), 2 cyclotomic a^2, 3 a^p, 4 a^(p^2),
-//   5 a^-1, 6 conj(a), 7 a^u (cyclotomic), 8 final exponentiation
-__global__ __launch_bounds__(64) void k_fp12_op(int op, const uint8_t* a, const uint8_t* b, int n, uint8_t* out) {
-  __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
-  Team T = make_team(lds, kTeamWords);
-  uint32_t* F = T.base + kSlots * kFp12Words;
-  int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
-  bool valid = idx < n;
-  int ci = valid ? idx : n - 1;
-  const int pos[6] = {5, 2, 4, 1, 3, 0};
-  if (T.active) {
-    Fp v;
-    bool ge;
-    fp_from_be(v, a + (size_t)ci * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0), &ge);
-    st_fp(slot(T, S_A) + T.e * 10, v);
-    fp_from_be(v, b + (size_t)ci * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0), &ge);
-    st_fp(slot(T, S_B) + T.e * 10, v);
-  }
-  team_sync();
-  {
-    Fp z, one;
-    fp_zero(z);
-    fp_one(one);
-    if (T.tl == 0) {
-      st_fp(F + R_ZERO * 10, z);
-      st_fp(F + R_ONE * 10, one);
-    }
-    team_sync();
-  }
-  // op bits 8..: repetitions (timing of one building block: reps - 1 extra
-  // applications feed the result back as the input)
-  int reps = (op >> 8) > 0 ? (op >> 8) : 1;
-  op &= 255;
-  for (int r = 0; r < reps; r++) {
-    if (r > 0) t12_copy(T, S_A, S_F);
-    switch (op) {  // kernel-uniform
-      case 0: t12_mul(T, S_F, S_A, S_B); break;
-      case 1: t12_sqr_fast(T, S_F, S_A); break;
-      case 2: t12_cyc_sqr(T, S_F, S_A); break;
-      case 3: t12_frob(T, S_F, S_A); break;
-      case 4: t12_frob2(T, S_F, S_A); break;
-      case 5: t12_inv(T, S_F, S_A, S_K, S_L); break;
-      case 6: t12_conj(T, S_F, S_A); break;
-      case 7: t12_pow_u_cyc(T, F, S_F, S_A); break;
-      case 8: t12_copy(T, S_F, S_A); team_final_exp(T, F); break;
-      case 9: t12_sqr_table(T, F, S_F, S_A); break;
-      case 10: t12_cyc_sqr_table(T, F, S_F, S_A); break;
-      default: t12_copy(T, S_F, S_A); break;
-    }
-  }
-  if (valid && T.active) {
-    Fp v;
-    ld_fp(v, slot(T, S_F) + T.e * 10);
-    fp_to_be(out + (size_t)idx * 384 + pos[T.k] * 64 + (T.comp ? 32 : 0), v);
-  }
-}
-
 // ------------------------------------------------------------------ aggregation
 // One 64-lane workgroup per request: lane l folds the registry points whose
 // bit i has i % 64 == l with mixed additions, then an LDS tree reduction
@@ -721,12 +390,6 @@ void launch_g1_mul(const PointG1* base, const uint8_t* scalars, int n, PointG1* 
 }
 void launch_hash_point(const uint32_t* k, PointG1* out, hipStream_t s) { k_hash_point<<<1, 64, 0, s>>>(k, out); }
 void launch_g2_lines(LineCoef* tab, hipStream_t s) { k_g2_lines<<<1, 64, 0, s>>>(tab); }
-void launch_verify(const CheckIn* in, int n, const LineCoef* tab, const PointG1* h, int32_t* codes, hipStream_t s) {
-  if (n > 0) k_verify<<<nblk(n, kTeamsPerBlock), 64, 0, s>>>(in, n, tab, h, codes);
-}
-void launch_pair(const PointG1* g1s, const PointG2* g2s, int n, const LineCoef* tab, uint8_t* gt, hipStream_t s) {
-  if (n > 0) k_pair<<<nblk(n, kTeamsPerBlock), 64, 0, s>>>(g1s, g2s, n, tab, gt);
-}
 void launch_aggregate(const PointG2* reg, int nreg, const AggRequest* reqs, int n, const uint64_t* words,
                       CheckIn* out, int32_t* codes, hipStream_t s) {
   if (n > 0) k_aggregate<<<n, 64, 0, s>>>(reg, nreg, reqs, n, words, out, codes);
@@ -748,19 +411,6 @@ void launch_extract_pk(const CheckIn* in, int n, PointG2* out, hipStream_t s) {
 }
 void launch_g2_combine(const PointG2* a, const PointG2* b, int n, PointG2* out, hipStream_t s) {
   if (n > 0) k_g2_combine<<<nblk(n, 64), 64, 0, s>>>(a, b, n, out);
-}
-void launch_fp12_op(int op, const uint8_t* a, const uint8_t* b, int n, uint8_t* out, hipStream_t s) {
-  if (n > 0) k_fp12_op<<<nblk(n, kTeamsPerBlock), 64, 0, s>>>(op, a, b, n, out);
-}
-int diag_read(uint64_t* out, size_t n) {
-#ifdef HG_DIAG
-  if (n > 4096 * 16) n = 4096 * 16;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
-#else
-  (void)out;
-  (void)n;
-  return -1;
-#endif
 }
 void launch_fp_mul(const uint32_t* a, const uint32_t* b, int n, uint32_t* out, hipStream_t s) {
   if (n > 0) k_fp_mul<<<nblk(n, 64), 64, 0, s>>>(a, b, n, out);

@@ -1,0 +1,211 @@
+// bn256_pairing.h — the team Miller loop and final exponentiation shared by
+// the pairing kernels (k_verify in bn256_verify.hip; k_pair and the Fp12 probe
+// in bn256_pair.hip). One 16-lane team per pairing check (bn256_team.h).
+#pragma once
+#include "bn256_kernels.h"
+#include "bn256_g2team.h"
+#include "bn256_xprog.h"
+
+namespace hg {
+
+// ------------------------------------------------------------------ diagnostics
+// Built only with -DHG_DIAG (tools/diag.py builds a separate library): lane 0
+// of every block accumulates s_memtime cycles per phase of k_verify.
+#if defined(HG_DIAG) && defined(HG_DIAG_TU)
+__shared__ uint64_t hg_diag_acc[16];
+extern __device__ uint64_t g_diag[4096 * 16];
+#define DIAG_T0() uint64_t diag_t0_ = __builtin_amdgcn_s_memtime()
+#define DIAG_ADD(k)                                                     \
+  do {                                                                  \
+    uint64_t diag_t1_ = __builtin_amdgcn_s_memtime();                   \
+    if (threadIdx.x == 0) hg_diag_acc[k] += diag_t1_ - diag_t0_;        \
+    diag_t0_ = diag_t1_;                                                \
+  } while (0)
+#else
+#define DIAG_T0() (void)0
+#define DIAG_ADD(k) (void)0
+#endif
+
+// ------------------------------------------------------------------ team Miller loop + final exp
+// LDS layout per team: 12 Fp12 slots followed by the per-check constants.
+static constexpr int kTeamWords = kSlots * kFp12Words + kG2Regs * 10;
+static constexpr int kTeamsPerBlock = 4;
+
+// the pairing's final exponentiation (x/crypto optate.go finalExponentiation)
+HG_DEV void team_final_exp(const Team& T, uint32_t* F) {
+  DIAG_T0();
+  t12_inv_x<S_A, S_F, S_K, S_L>(T);  // A = f^-1
+  DIAG_ADD(5);
+  t12_conj(T, S_B, S_F);           // B = conj(f)
+  x_mul12<S_F, S_B, S_A>(T);       // t1 = f^(p^6 - 1)
+  t12_frob2(T, S_A, S_F);
+  x_mul12<S_F, S_F, S_A>(T);       // t1 = t1^(p^2 + 1)
+  t12_frob(T, S_A, S_F);           // fp
+  t12_frob2(T, S_B, S_F);          // fp2
+  x_mul12<S_A, S_A, S_B>(T);
+  t12_frob(T, S_B, S_B);           // fp3
+  x_mul12<S_A, S_A, S_B>(T);       // y0 = fp * fp2 * fp3
+  DIAG_ADD(6);
+  t12_pow_u_x<S_C, S_F>(T);       // fu
+  t12_pow_u_x<S_D, S_C>(T);       // fu2
+  t12_pow_u_x<S_E, S_D>(T);       // fu3
+  DIAG_ADD(7);
+  t12_frob(T, S_G, S_C);
+  t12_conj(T, S_G, S_G);           // y3 = conj(frob(fu))
+  t12_frob(T, S_H, S_D);
+  x_mul12<S_H, S_C, S_H>(T);
+  t12_conj(T, S_H, S_H);           // y4 = conj(fu * frob(fu2))
+  t12_frob2(T, S_C, S_D);          // y2 = frob2(fu2)
+  t12_conj(T, S_D, S_D);           // y5 = conj(fu2)
+  t12_frob(T, S_I, S_E);
+  x_mul12<S_I, S_E, S_I>(T);
+  t12_conj(T, S_I, S_I);           // y6 = conj(fu3 * frob(fu3))
+  x_cyc_sqr<S_K, S_I>(T);
+  x_mul12<S_K, S_K, S_H>(T);
+  x_mul12<S_K, S_K, S_D>(T);       // t0 = y6^2 y4 y5
+  x_mul12<S_J, S_G, S_D>(T);
+  x_mul12<S_J, S_J, S_K>(T);       // t1 = y3 y5 t0
+  x_mul12<S_K, S_K, S_C>(T);       // t0 = t0 y2
+  x_cyc_sqr<S_J, S_J>(T);
+  x_mul12<S_J, S_J, S_K>(T);
+  x_cyc_sqr<S_J, S_J>(T);            // t1 = (t1^2 t0)^2
+  t12_conj(T, S_L, S_F);           // y1 = conj(t1_easy)
+  x_mul12<S_K, S_J, S_L>(T);       // t0 = t1 y1
+  x_mul12<S_J, S_J, S_A>(T);       // t1 = t1 y0
+  x_cyc_sqr<S_K, S_K>(T);
+  x_mul12<S_F, S_K, S_J>(T);       // result
+  DIAG_ADD(6);
+}
+
+// Per-check inputs of the team Miller loop.
+struct CheckCtx {
+  Fp2 qx, qy;   // affine pk (a dummy valid point when the pk is infinity)
+  Fp hx, hy;    // H (affine)
+  Fp sx, sy;    // sig (affine)
+  bool use_q;   // pk contributes (not infinity)
+  bool use_s;   // sig contributes (not infinity)
+};
+
+// Writes the team's G2 register file: point R = (Q, 1, 1), Q, -Qy, Qy^2, the
+// Frobenius images q1 = pi(Q), -q2 = (Qx gamma2[2], Qy) (optate.go miller),
+// the G1 points and constants.
+HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
+  const Fp2 g1[6] = HG_GAMMA1;
+  const Fp g2[6] = HG_GAMMA2;
+  Fp2 nqy, r2, q1x, q1y, q1r2, q2x, t, one2, zero2;
+  f2_neg(nqy, C.qy);
+  f2_sqr(r2, C.qy);
+  f2_conj(t, C.qx);
+  f2_mul(q1x, t, g1[2]);
+  f2_conj(t, C.qy);
+  f2_mul(q1y, t, g1[3]);
+  f2_sqr(q1r2, q1y);
+  f2_muls(q2x, C.qx, g2[2]);
+  f2_one(one2);
+  f2_zero(zero2);
+  Fp zero, one, nsy;
+  fp_zero(zero);
+  fp_one(one);
+  fp_neg(nsy, C.sy);
+  if (T.tl == 0) {
+    auto put2 = [&](int rx, const Fp2& v) {
+      st_fp(F + rx * 10, v.x);
+      st_fp(F + (rx + 1) * 10, v.y);
+    };
+    st_fp(F + R_ZERO * 10, zero);
+    st_fp(F + R_ONE * 10, one);
+    st_fp(F + R_PX * 10, C.hx);
+    st_fp(F + R_PY * 10, C.hy);
+    st_fp(F + R_SX * 10, C.sx);
+    st_fp(F + R_NSY * 10, nsy);
+    put2(R_X_x, C.qx);
+    put2(R_Y_x, C.qy);
+    put2(R_Z_x, one2);
+    put2(R_T_x, one2);
+    put2(R_QX_x, C.qx);
+    put2(R_QY_x, C.qy);
+    put2(R_NQY_x, nqy);
+    put2(R_R2_x, r2);
+    put2(R_P1X_x, q1x);
+    put2(R_P1Y_x, q1y);
+    put2(R_P1R2_x, q1r2);
+    put2(R_P2X_x, q2x);
+    put2(R_F2ONE_x, one2);
+    put2(R_F2ZERO_x, zero2);
+  }
+  team_sync();
+}
+
+// Loads the G2Base line s (a, bx, cy: 6 Fp) into FA, FBX, FCY.
+HG_DEV void load_fixed_line(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
+  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
+  if (T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
+  team_sync();
+}
+
+// A point at infinity contributes the unit line (a = b = 0, c = 1): after the
+// G2 program, teams with an infinite pk (sig) overwrite LA, LB, LC (FA, FB,
+// FC); the branch is taken only when some team of the wave needs it.
+HG_DEV void unit_lines(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed) {
+  const bool fix_q = !C.use_q, fix_s = has_fixed && !C.use_s;
+  if (__ballot(fix_q || fix_s) == 0) return;  // wave-uniform
+  Fp z, o;
+  fp_zero(z);
+  fp_one(o);
+  if (T.tl < 6) {
+    // element tl of (a.x, a.y, b.x, b.y, c.x, c.y); c.y is the real part of c
+    Fp v;
+    fp_sel(v, T.tl == 5, o, z);
+    const int fr = T.tl < 2 ? R_FA_x + T.tl : (T.tl < 4 ? R_FB_x + T.tl - 2 : R_FC_x + T.tl - 4);
+    if (fix_q) st_fp(F + (R_LA_x + T.tl) * 10, v);  // LA, LB, LC are consecutive
+    if (fix_s) st_fp(F + fr * 10, v);
+  }
+  team_sync();
+}
+
+// f *= pk line (LA, LB, LC) and, when has_fixed, the G2Base line (FA, FB, FC)
+HG_DEV void apply_lines(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed) {
+  unit_lines(T, F, C, has_fixed);
+  x_line_pk<S_F, S_F>(T);
+  if (has_fixed) x_line_fix<S_F, S_F>(T);
+}
+
+// f = Miller(pk at H) * Miller(G2Base at -sig) (x/crypto optate.go miller, with
+// the two loops sharing their squarings); the G2 steps run as team programs.
+HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, const LineCoef* tab, bool has_fixed) {
+  const int8_t naf[kNafLen] = HG_NAF;
+  t12_set_one(T, S_F);
+  g2_regs_init(T, F, C);
+  int s = 0;
+  DIAG_T0();
+  for (int i = kNafLen - 1; i > 0; i--) {
+    load_fixed_line(T, F, tab, s++);
+    DIAG_ADD(0);
+    x_g2<XP_DBL>(T);
+    DIAG_ADD(1);
+    if (i != kNafLen - 1) x_sqr12<S_F, S_F>(T);
+    DIAG_ADD(2);
+    apply_lines(T, F, C, has_fixed);
+    DIAG_ADD(3);
+    int d = naf[i - 1];
+    if (d != 0) {
+      load_fixed_line(T, F, tab, s++);
+      DIAG_ADD(0);
+      if (d > 0) x_g2<XP_ADD_POS>(T);
+      else x_g2<XP_ADD_NEG>(T);
+      DIAG_ADD(4);
+      apply_lines(T, F, C, has_fixed);
+      DIAG_ADD(3);
+    }
+  }
+  load_fixed_line(T, F, tab, s++);
+  x_g2<XP_ADD_F1>(T);
+  apply_lines(T, F, C, has_fixed);
+  load_fixed_line(T, F, tab, s++);
+  x_g2<XP_ADD_F2>(T);
+  apply_lines(T, F, C, has_fixed);
+}
+
+HG_DEV uint32_t* team_regs(const Team& T) { return T.base + kSlots * kFp12Words; }
+
+}  // namespace hg

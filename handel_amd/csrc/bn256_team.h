@@ -18,6 +18,8 @@
 namespace hg {
 
 static constexpr int kFp12Words = 120;  // 12 elements x 10 limbs
+// Fp12 slots of a team's LDS region (tools/gen_g2_schedule.py SLOTS uses the same order)
+enum { S_F = 0, S_A, S_B, S_C, S_D, S_E, S_G, S_H, S_I, S_J, S_K, S_L, kSlots };
 
 struct Team {
   uint32_t* base;  // this team's LDS slots
@@ -409,11 +411,9 @@ HG_DEV void f6_inv_lane(Fp2& r0, Fp2& r1, Fp2& r2, const Fp2& c0, const Fp2& c1,
   f2_mul(r2, t2, d);
 }
 
-// dst = a^-1 using scratch slots s1, s2 (x/crypto gfP12.Invert)
-HG_DEV void t12_inv(const Team& T, int dst, int sa, int s1, int s2) {
-  t12_conj(T, s1, sa);          // s1 = conj(a)
-  t12_mul(T, s2, sa, s1);       // s2 = a*conj(a) = N (even coefficients only)
-  // every lane inverts N (an Fp6 element over tau = w^2) redundantly
+// slot s2 holds N = a conj(a) (an Fp6 element over tau = w^2: odd coefficients
+// zero); replaces it by N^-1. Every lane inverts N redundantly.
+HG_DEV void t12_inv_norm(const Team& T, int s2) {
   Fp2 n0, n1, n2;
   ld_f2(n0, slot(T, s2), 0);
   ld_f2(n1, slot(T, s2), 2);
@@ -433,7 +433,14 @@ HG_DEV void t12_inv(const Team& T, int dst, int sa, int s1, int s2) {
     if (T.active) st_fp(slot(T, s2) + T.e * 10, e);
   }
   team_sync();
-  t12_mul(T, dst, s1, s2);  // conj(a) / N
+}
+
+// dst = a^-1 using scratch slots s1, s2 (x/crypto gfP12.Invert)
+HG_DEV void t12_inv(const Team& T, int dst, int sa, int s1, int s2) {
+  t12_conj(T, s1, sa);          // s1 = conj(a)
+  t12_mul(T, s2, sa, s1);       // s2 = a*conj(a) = N (even coefficients only)
+  t12_inv_norm(T, s2);
+  t12_mul(T, dst, s1, s2);      // conj(a) / N
 }
 
 // dst = a^u (x/crypto gfP12.Exp with the BN parameter u), dst != sa

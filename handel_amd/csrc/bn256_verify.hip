@@ -1,0 +1,89 @@
+// bn256_verify.hip — k_verify: the batched pairing check
+// e(H, pk) * e(-sig, G2Base) == 1 (PublicKey.VerifySignature, bn256/go/bn256.go:82-94),
+// one 16-lane team per check, TEAMS teams per single-wave workgroup.
+#define HG_DIAG_TU 1
+#include <cstdlib>
+#include <hip/hip_runtime.h>
+
+#include "bn256_pairing.h"
+
+namespace hg {
+static inline int nblk(int n, int b) { return (n + b - 1) / b; }
+
+#ifdef HG_DIAG
+__device__ uint64_t g_diag[4096 * 16];
+#endif
+
+
+// TEAMS checks per workgroup of 16 * TEAMS lanes (one wave; LDS sized to TEAMS)
+template <int TEAMS>
+__global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const LineCoef* tab,
+                                               const PointG1* hpt, int32_t* codes) {
+  __shared__ uint32_t lds[TEAMS * kTeamWords];
+  Team T = make_team(lds, kTeamWords);
+  uint32_t* F = team_regs(T);
+  int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
+  bool valid = idx < n;
+  int ci = valid ? idx : n - 1;
+  const CheckIn& I = in[ci];
+  CheckCtx C;
+  C.qx = I.pk.x;
+  C.qy = I.pk.y;
+  C.hx = hpt->x;
+  C.hy = hpt->y;
+  C.sx = I.sig.x;
+  C.sy = I.sig.y;
+  C.use_q = I.pk.inf == 0;
+  C.use_s = I.sig.inf == 0;
+  if (!C.use_q) {  // keep the (unused) doubling chain well-defined
+    const Fp2 gx = HG_G2X, gy = HG_G2Y;
+    C.qx = gx;
+    C.qy = gy;
+  }
+#ifdef HG_DIAG
+  if (threadIdx.x < 16) hg_diag_acc[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t diag_start = __builtin_amdgcn_s_memtime();
+#endif
+  team_miller_check(T, F, C, tab, true);
+#ifdef HG_DIAG
+  uint64_t diag_mid = __builtin_amdgcn_s_memtime();
+#endif
+  team_final_exp(T, F);
+  bool ok = t12_is_one(T, S_F);
+  if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
+#ifdef HG_DIAG
+  uint64_t diag_end = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {
+    for (int k = 0; k < 8; k++) g_diag[blockIdx.x * 16 + k] = hg_diag_acc[k];
+    g_diag[blockIdx.x * 16 + 8] = diag_mid - diag_start;
+    g_diag[blockIdx.x * 16 + 9] = diag_end - diag_mid;
+    g_diag[blockIdx.x * 16 + 10] = diag_end - diag_start;
+  }
+#endif
+}
+
+
+void launch_verify(const CheckIn* in, int n, const LineCoef* tab, const PointG1* h, int32_t* codes, hipStream_t s) {
+  // HG_TEAMS_PER_BLOCK (diagnostic): fewer checks per wave -> more waves per SIMD
+  static const int tpb = [] {
+    const char* e = getenv("HG_TEAMS_PER_BLOCK");
+    int v = e ? atoi(e) : kTeamsPerBlock;
+    return (v >= 1 && v <= kTeamsPerBlock) ? v : kTeamsPerBlock;
+  }();
+  if (n <= 0) return;
+  if (tpb == 4) k_verify<4><<<nblk(n, 4), 64, 0, s>>>(in, n, tab, h, codes);
+  else if (tpb == 2) k_verify<2><<<nblk(n, 2), 32, 0, s>>>(in, n, tab, h, codes);
+  else k_verify<1><<<n, 16, 0, s>>>(in, n, tab, h, codes);
+}
+int diag_read(uint64_t* out, size_t n) {
+#ifdef HG_DIAG
+  if (n > 4096 * 16) n = 4096 * 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+#else
+  (void)out;
+  (void)n;
+  return -1;
+#endif
+}
+}  // namespace hg

@@ -1,0 +1,195 @@
+// bn256_xprog.h — executor for the generated two-phase team programs
+// (tables: bn256_xtab.h, from tools/gen_g2_schedule.py).
+//
+// A round makes every lane of a 16-lane team compute one Fp element
+//     dst = REDC( sum_p U_p * V_p  +  R * sum_l lin_l )
+// where U_p, V_p are Fp elements read from the team's LDS and lin_l are small
+// multiples of Fp elements (the "x 1" slots of a program, added into the high
+// columns so that REDC returns them unchanged). Operands that are linear
+// combinations of several elements are materialised once per team by a
+// pre-pass (phase 1): each lane evaluates up to NV of the round's distinct
+// combinations into a scratch area, so the product phase (phase 2) is pure
+// v_mad_u64_u32 work on LDS operands — no per-limb selects, no coefficient
+// multiplies, no carries.
+//
+// Pre-pass terms are k * x (k > 0) or k * (2p - x) (k < 0: "negated"), summed
+// limb-wise without carries: (2p)'' below is 2p with limbs in [2^26, 2^27 + 2^26)
+// (top limb 2 p_9 - 1), so (2p)''_l - x_l >= 0 for every canonical x. The
+// generator bounds every limb sum below 2^32, every 64-bit column below 2^64
+// and every REDC input below 800 p^2 (acc_reduce_wide's exact range, < 31 p
+// after REDC).
+//
+// Every table is bound to one call site: operands are absolute positions in
+// the team region (Fp12 slot s element e -> element 12 s + e, register r ->
+// element 144 + r), so an address is one add.
+#pragma once
+#include <utility>
+
+#include "bn256_team.h"
+
+namespace hg {
+
+struct Team;
+template <int NV, int NT, int NP, int NL, int W>
+HG_DEV void x_round(const Team& T, const uint32_t* tab);
+
+}  // namespace hg
+
+#include "bn256_xtab.h"
+
+namespace hg {
+
+static constexpr uint32_t kP2N[10] = {HG_P2N};
+
+template <int... I, typename Fn>
+HG_DEV void x_static_for(std::integer_sequence<int, I...>, Fn&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+HG_DEV void x_for(Fn&& f) {
+  x_static_for(std::make_integer_sequence<int, N>{}, f);
+}
+
+// 16-bit table entries: operands and destinations are byte offsets into the
+// team region (0xffff = none); a linear term is element index << 8 | (int8) coef.
+template <int W>
+HG_DEV uint32_t x_half(const uint32_t (&w)[W], int i) {
+  return (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xffffu);
+}
+template <int W>
+HG_DEV uint32_t x_off(const uint32_t (&w)[W], int i) {
+  return x_half(w, i);
+}
+template <int W>
+HG_DEV uint32_t x_term_off(const uint32_t (&w)[W], int i) {
+  return (x_half(w, i) >> 8) * 40u;
+}
+template <int W>
+HG_DEV int32_t x_coef(const uint32_t (&w)[W], int i) {
+  return (int32_t)(int8_t)(x_half(w, i) & 255u);
+}
+HG_DEV uint32_t* x_at(const Team& T, uint32_t byte_off) {
+  return (uint32_t*)__builtin_assume_aligned((uint8_t*)T.base + byte_off, 8);
+}
+
+// Evaluates sum_t c_t * x_t (+ K (2p)'' with K = sum of |c_t| over the negative
+// c_t, so every limb is a non-negative exact sum) into acc[10] as 32-bit limbs:
+// one v_mad_i64_i32 per limb and term, the correction once per value.
+template <int W, int NT>
+HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t (&out)[10]) {
+  int64_t acc[10];
+#pragma unroll
+  for (int l = 0; l < 10; l++) acc[l] = 0;
+  int32_t negk = 0;
+  x_for<NT>([&](auto t) {
+    const uint32_t off = x_term_off(w, base + t);
+    const int32_t c = x_coef(w, base + t);
+    const uint32_t* x = x_at(T, off);
+    negk += c < 0 ? -c : 0;
+#pragma unroll
+    for (int l = 0; l < 10; l++) acc[l] += (int64_t)c * (int32_t)x[l];
+  });
+#pragma unroll
+  for (int l = 0; l < 10; l++) out[l] = (uint32_t)acc[l] + (uint32_t)negk * kP2N[l];
+}
+
+// One round. Table layout per lane (16-bit entries): NV x (dst, NT x term),
+// NP x (u, v), NL x term, dst; padded to W dwords.
+template <int NV, int NT, int NP, int NL, int W>
+HG_DEV void x_round(const Team& T, const uint32_t* tab) {
+  uint32_t w[W];
+  const uint32_t* my = tab + T.tl * W;
+  x_for<W>([&](auto i) { w[i] = my[i]; });
+  if constexpr (NV > 0) {
+    x_for<NV>([&](auto v) {
+      constexpr int base = v * (1 + NT);
+      const uint32_t dst = x_off(w, base);
+      uint32_t val[10];
+      x_lincomb<W, NT>(T, w, base + 1, val);
+      if (dst != 0xffffu) {
+        uint32_t* o = x_at(T, dst);
+#pragma unroll
+        for (int l = 0; l < 10; l++) o[l] = val[l];
+      }
+    });
+    team_sync();
+  }
+  constexpr int pbase = NV * (1 + NT);
+  Acc acc;
+  acc_zero(acc);
+  x_for<NP>([&](auto p) {
+    Fp a, b;
+    ld_fp(a, x_at(T, x_off(w, pbase + 2 * p)));
+    ld_fp(b, x_at(T, x_off(w, pbase + 2 * p + 1)));
+    acc_mad(acc, a, b);
+  });
+  constexpr int lbase = pbase + 2 * NP;
+  if constexpr (NL > 0) {
+    uint32_t val[10];
+    x_lincomb<W, NL>(T, w, lbase, val);
+#pragma unroll
+    for (int l = 0; l < 10; l++) acc.c[10 + l] += val[l];
+  }
+  const uint32_t dst = x_off(w, lbase + NL);
+  Fp r;
+  acc_reduce_wide(r, acc);
+  team_sync();
+  if (dst != 0xffffu) st_fp(x_at(T, dst), r);
+  team_sync();
+}
+
+// ------------------------------------------------------------------ call-site wrappers
+// dst = a * b (Fp12)
+template <int D, int A, int B>
+HG_DEV void x_mul12(const Team& T) { XInst<XP_MUL12, D, A, B>::run(T); }
+// dst = a^2 for a in the cyclotomic subgroup (Granger-Scott)
+template <int D, int A>
+HG_DEV void x_cyc_sqr(const Team& T) { XInst<XP_CYC_SQR_X, D, A>::run(T); }
+// dst = a^2 (Miller loop)
+template <int D, int A>
+HG_DEV void x_sqr12(const Team& T) { XInst<XP_SQR12, D, A>::run(T); }
+// dst = a * (LC + LB w + LA w^3) / a * (FC + FB w + FA w^3): the pk / G2Base lines
+template <int D, int A>
+HG_DEV void x_line_pk(const Team& T) { XInst<XP_LINE_PK, D, A>::run(T); }
+template <int D, int A>
+HG_DEV void x_line_fix(const Team& T) { XInst<XP_LINE_FIX, D, A>::run(T); }
+// G2 Miller-loop steps on the register file (x/crypto lineFunctionDouble / Add)
+template <int PROG>
+HG_DEV void x_g2(const Team& T) { XInst<PROG>::run(T); }
+
+
+__constant__ static const int8_t kUNaf3X[kUNaf3Len] = HG_U_NAF3;
+
+// dst = a^u (x/crypto gfP12.Exp(t, u)) for a in the cyclotomic subgroup, where
+// a^-1 = conj(a): width-3 signed digits of u (62 cyclotomic squarings and 16
+// multiplications instead of 62 + 29). Scratch slots: J = a^3, K = a^-1,
+// L = a^-3 (dst, SA not among them).
+template <int D, int SA>
+HG_DEV void t12_pow_u_x(const Team& T) {
+  static_assert(D != S_J && D != S_K && D != S_L && SA != S_J && SA != S_K && SA != S_L, "scratch slots");
+  static_assert(HG_U_NAF3_TOP == 3, "top digit of the width-3 NAF of u");
+  x_cyc_sqr<S_J, SA>(T);
+  x_mul12<S_J, S_J, SA>(T);  // a^3
+  t12_conj(T, S_K, SA);      // a^-1
+  t12_conj(T, S_L, S_J);     // a^-3
+  t12_copy(T, D, S_J);
+  for (int i = kUNaf3Len - 2; i >= 0; i--) {
+    x_cyc_sqr<D, D>(T);
+    const int d = kUNaf3X[i];  // wave-uniform
+    if (d == 1) x_mul12<D, D, SA>(T);
+    else if (d == 3) x_mul12<D, D, S_J>(T);
+    else if (d == -1) x_mul12<D, D, S_K>(T);
+    else if (d == -3) x_mul12<D, D, S_L>(T);
+  }
+}
+
+// dst = a^-1 (x/crypto gfP12.Invert) with scratch slots S1, S2
+template <int DST, int SA, int S1, int S2>
+HG_DEV void t12_inv_x(const Team& T) {
+  t12_conj(T, S1, SA);          // S1 = conj(a)
+  x_mul12<S2, SA, S1>(T);       // S2 = a conj(a) = N (even coefficients only)
+  t12_inv_norm(T, S2);          // S2 = N^-1
+  x_mul12<DST, S1, S2>(T);      // conj(a) / N
+}
+
+}  // namespace hg

@@ -241,6 +241,52 @@ def prog_cyc_sqr():
     return [lanes]
 
 
+def prog_cyc_sqr_x():
+    """Granger-Scott squaring with at most 3 products per lane (the operand
+    combinations are shared by the team's pre-pass): per group (a, b),
+        3(a^2 + xi b^2).x = (6ax) ay + (18bx) by + 3(by + bx)(by - bx)
+        3(a^2 + xi b^2).y = 3(ay + ax)(ay - ax) - (6bx) by + 9(by + bx)(by - bx)
+        6ab = (6ax by + 6ay bx) i + (6ay by - 6ax bx)
+        6 xi ab = (6(3ax + ay) by + 6(3ay - ax) bx) i + (6(3ay - ax) by - 6(3ax + ay) bx)
+    plus -2c (squared lanes) or +2c (product lanes) as a linear term."""
+    def e(name, c):
+        return comp(name, c)
+
+    lanes = []
+    groups = {0: ("A0", "A3"), 1: ("A1", "A4"), 2: ("A2", "A5")}
+    # output coefficient k -> (group, kind): sq = a^2 + xi b^2 part, ab = 2ab part, xi = 2 xi ab part
+    kinds = {0: (0, "sq"), 3: (0, "ab"), 2: (1, "sq"), 5: (1, "ab"), 4: (2, "sq"), 1: (2, "xi")}
+    for k in range(6):
+        g, kind = kinds[k]
+        a, b = groups[g]
+        ax, ay, bx, by = e(a, "x"), e(a, "y"), e(b, "x"), e(b, "y")
+        for c in "xy":
+            if kind == "sq":
+                if c == "x":
+                    slots = [([(ax, 6)], [(ay, 1)]), ([(bx, 18)], [(by, 1)]),
+                             ([(by, 3), (bx, 3)], [(by, 1), (bx, -1)])]
+                else:
+                    slots = [([(ay, 3), (ax, 3)], [(ay, 1), (ax, -1)]), ([(bx, -6)], [(by, 1)]),
+                             ([(by, 9), (bx, 9)], [(by, 1), (bx, -1)])]
+                lin = [(e(f"A{k}", c), -2)]
+            elif kind == "ab":
+                if c == "x":
+                    slots = [([(ax, 6)], [(by, 1)]), ([(ay, 6)], [(bx, 1)])]
+                else:
+                    slots = [([(ay, 6)], [(by, 1)]), ([(ax, -6)], [(bx, 1)])]
+                lin = [(e(f"A{k}", c), 2)]
+            else:
+                u = [(ax, 18), (ay, 6)]
+                v = [(ay, 18), (ax, -6)]
+                if c == "x":
+                    slots = [(u, [(by, 1)]), (v, [(bx, 1)])]
+                else:
+                    slots = [(v, [(by, 1)]), (u, [(bx, -1)])]
+                lin = [(e(f"A{k}", c), 2)]
+            lanes.append(Lane(comp(f"D{k}", c), slots + [(lin, one())]))
+    return [lanes]
+
+
 def prog_sqr12():
     """f^2 in Fp2[w]/(w^6 - xi): c_k = sum_{i<=j, i+j = k mod 6} (2 - [i==j]) a_i a_j xi^[i+j>=6]."""
     def xi_prod(i, j, c, mult):
@@ -271,6 +317,54 @@ def prog_sqr12():
     return [lanes]
 
 
+def xi_lc(lx, ly):
+    """components of xi * (lx i + ly) for Fp lincombs lx, ly: (3lx + ly, 3ly - lx)."""
+    return add(scale(lx, 3), ly), add(scale(ly, 3), neg(lx))
+
+
+def prog_mul12():
+    """dst = A * B in Fp2[w]/(w^6 - xi): lane (k, c) sums over i the component c of
+    A_i' B_j, j = k - i mod 6, A_i' = xi A_i when k - i < 0 (x/crypto gfP12.Mul)."""
+    lanes = []
+    for k in range(6):
+        for c in "xy":
+            slots = []
+            for i in range(6):
+                j = (k - i) % 6
+                ax, ay = [(comp(f"A{i}", "x"), 1)], [(comp(f"A{i}", "y"), 1)]
+                if k - i < 0:
+                    ax, ay = xi_lc(ax, ay)
+                bx, by = [(comp(f"B{j}", "x"), 1)], [(comp(f"B{j}", "y"), 1)]
+                if c == "x":
+                    slots += [(ax, by), (ay, bx)]
+                else:
+                    slots += [(ay, by), (neg(ax), bx)]
+            lanes.append(Lane(comp(f"D{k}", c), slots))
+    return [lanes]
+
+
+def prog_line(la, lb, lc):
+    """dst = A * (lc + lb w + la w^3) (sparse line, coefficients in F registers);
+    xi is applied to the line coefficient of a wrapped term."""
+    lanes = []
+    for k in range(6):
+        for c in "xy":
+            slots = []
+            for jpos, L in ((0, lc), (1, lb), (3, la)):
+                i = k - jpos
+                lx, ly = [(comp(L, "x"), 1)], [(comp(L, "y"), 1)]
+                if i < 0:
+                    i += 6
+                    lx, ly = xi_lc(lx, ly)
+                fx, fy = [(comp(f"A{i}", "x"), 1)], [(comp(f"A{i}", "y"), 1)]
+                if c == "x":
+                    slots += [(fx, ly), (fy, lx)]
+                else:
+                    slots += [(fy, ly), (fx, neg(lx))]
+            lanes.append(Lane(comp(f"D{k}", c), slots))
+    return [lanes]
+
+
 PROGRAMS = {
     "DBL": prog_double(),
     "ADD_POS": prog_add("QX", "QY", "R2"),
@@ -279,7 +373,13 @@ PROGRAMS = {
     "ADD_F2": prog_add("P2X", "QY", "R2"),
     "CYC_SQR": prog_cyc_sqr(),
     "SQR12": prog_sqr12(),
+    "MUL12": prog_mul12(),
+    "LINE_PK": prog_line("LA", "LB", "LC"),
+    "LINE_FIX": prog_line("FA", "FB", "FC"),
+    "CYC_SQR_X": prog_cyc_sqr_x(),
 }
+# programs also emitted in the single-phase table format (bn256_g2sched.h)
+LEGACY = ("DBL", "ADD_POS", "ADD_NEG", "ADD_F1", "ADD_F2", "CYC_SQR", "SQR12")
 
 
 # ------------------------------------------------------------------ checks + interpreter
@@ -331,6 +431,8 @@ def validate(seed=1):
 
     rng = random.Random(seed)
     for name, prog in PROGRAMS.items():
+        if name not in LEGACY:
+            continue
         for i, r in enumerate(prog):
             check_round(r, f"{name}[{i}]")
     for trial in range(3):
@@ -376,6 +478,425 @@ def validate(seed=1):
     return True
 
 
+# ------------------------------------------------------------------ two-phase compilation (bn256_xprog.h)
+# New operand space: 0..127 F, 128..143 slot A, 144..159 slot B, 160.. scratch.
+X_SLOT_B = 144
+X_SCR = 160
+P_LIMB_TOP = P >> 234
+
+
+def _p2n_limbs():
+    """(2p)'': 2p re-spread so limb l >= 2^26 (l < 9) and the top limb is 2 p_9 - 1."""
+    q = [((2 * P) >> (26 * l)) & ((1 << 26) - 1) for l in range(9)] + [(2 * P) >> 234]
+    out = [q[0] + (1 << 26)] + [q[l] + (1 << 26) - 1 for l in range(1, 9)] + [q[9] - 1]
+    assert sum(v << (26 * l) for l, v in enumerate(out)) == 2 * P
+    return out
+
+
+P2N = _p2n_limbs()
+CANON_LIMB = [(1 << 26) - 1] * 9 + [P_LIMB_TOP]      # limb bounds of a canonical element
+NEG_LIMB = list(P2N)                                 # limb bounds of (2p)'' - x
+
+
+def _xsrc(r):
+    """old register code -> new operand code"""
+    if r >= SLOT_B:
+        return X_SLOT_B + (r - SLOT_B)
+    return r
+
+
+class XRound:
+    def __init__(self, nv, nt, np_, nl, lanes, name):
+        self.nv, self.nt, self.np, self.nl, self.lanes, self.name = nv, nt, np_, nl, lanes, name
+
+    def words(self):
+        nhalves = self.nv * (1 + self.nt) + 2 * self.np + self.nl + 1
+        return (nhalves + 1) // 2
+
+    def lane_halves(self, t):
+        """16-bit entries for bound rounds (bn256_xprog.h): operands/destinations
+        as byte offsets (0xffff none), terms as element << 8 | int8 coef."""
+        L = self.lanes[t]
+        h = []
+        off = lambda e: 0xFFFF if e == NONE else 40 * e  # noqa: E731
+        for dst, terms in L["pre"]:
+            h.append(off(dst))
+            for src, c in terms:
+                assert -128 <= c <= 127
+                h.append((src << 8) | (c & 255))
+        for u, v in L["prod"]:
+            h += [off(u), off(v)]
+        for src, c in L["lin"]:
+            h.append((src << 8) | (c & 255))
+        h.append(off(L["dst"]))
+        h += [0] * (2 * self.words() - len(h))
+        return h
+
+    def lane_bytes(self, t):
+        L = self.lanes[t]
+        b = []
+        for dst, terms in L["pre"]:
+            b.append(dst)
+            for src, c in terms:
+                b += [src, c & 255]
+        for u, v in L["prod"]:
+            b += [u, v]
+        for src, c in L["lin"]:
+            b += [src, c & 255]
+        b.append(L["dst"])
+        b += [0] * (4 * self.words() - len(b))
+        return b
+
+
+def compile_round(lanes, name, scratch_cap):
+    one_lc = [(REG["ONE"], 1)]
+    values = {}      # canonical lincomb -> scratch code
+    order = []
+
+    def operand(lc):
+        lc = [(r, k) for r, k in lc if k != 0] or [(REG["ZERO"], 1)]
+        if len(lc) == 1 and lc[0][1] == 1:
+            return _xsrc(lc[0][0])
+        key = tuple(sorted((_xsrc(r), k) for r, k in lc))
+        if key not in values:
+            values[key] = X_SCR + len(order)
+            order.append(key)
+        return values[key]
+
+    per_lane = []
+    for l in lanes:
+        prods, lins = [], []
+        for a, b in l.slots:
+            if list(b) == one_lc:
+                lins += [(_xsrc(r), k) for r, k in a if k != 0]
+            elif list(a) == one_lc:
+                lins += [(_xsrc(r), k) for r, k in b if k != 0]
+            else:
+                prods.append((operand(a), operand(b)))
+        per_lane.append((l.dst, prods, lins))
+    assert len(per_lane) <= 16, name
+    nvals = len(order)
+    assert nvals <= scratch_cap, f"{name}: {nvals} pre-pass values > scratch {scratch_cap}"
+    nv = (nvals + 15) // 16
+    nt = max([len(k) for k in order] or [0])
+    np_ = max(len(p) for _, p, _ in per_lane)
+    nl = max(len(q) for _, _, q in per_lane)
+    zero = REG["ZERO"]
+    out = []
+    for t in range(16):
+        pre = []
+        for v in range(nv):
+            vi = t + 16 * v
+            if vi < nvals:
+                terms = list(order[vi]) + [(zero, 0)] * (nt - len(order[vi]))
+                pre.append((X_SCR + vi, terms))
+            else:
+                pre.append((NONE, [(zero, 0)] * nt))
+        if t < len(per_lane):
+            dst, prods, lins = per_lane[t]
+        else:
+            dst, prods, lins = NONE, [], []
+        prods = prods + [(zero, zero)] * (np_ - len(prods))
+        lins = lins + [(zero, 0)] * (nl - len(lins))
+        out.append({"pre": pre, "prod": prods, "lin": lins, "dst": dst})
+    xr = XRound(nv, nt, np_, nl, out, name)
+    check_xround(xr, order)
+    return xr
+
+
+def check_xround(xr, order):
+    """Limb sums < 2^32, 64-bit columns < 2^64, REDC input < 800 p^2."""
+    def src_bound(code):
+        if code >= X_SCR:
+            return vbound[code]
+        return (P, CANON_LIMB)
+
+    vbound = {}
+    for i, key in enumerate(order):
+        val, limbs = 0, [0] * 10
+        for src, k in key:
+            v, lb = src_bound(src)
+            if k < 0:
+                v, lb = 2 * P, NEG_LIMB
+            val += abs(k) * v
+            limbs = [a + abs(k) * b for a, b in zip(limbs, lb)]
+        assert max(limbs) < 1 << 32, f"{xr.name}: pre-pass limb overflow {key}"
+        vbound[X_SCR + i] = (val, limbs)
+    for L in xr.lanes:
+        T, cols = 0, [0] * 20
+        for u, v in L["prod"]:
+            (bu, lu), (bv, lv) = src_bound(u), src_bound(v)
+            T += bu * bv
+            for i in range(10):
+                for j in range(10):
+                    cols[i + j] += lu[i] * lv[j]
+        for src, k in L["lin"]:
+            b, lb = src_bound(src)
+            if k < 0:
+                b, lb = 2 * P, NEG_LIMB
+            T += abs(k) * b * (1 << 260)
+            for i in range(10):
+                cols[10 + i] += abs(k) * lb[i]
+        assert max(cols) < 1 << 64, f"{xr.name}: column overflow"
+        # REDC(T) < T/R + p; fp_reduce8 is exact for inputs below 31 p (q <= 30 keeps
+        # q * p_l inside int32), so T < 800 p^2 (T/R < 28.3 p) leaves a margin
+        assert T < 800 * P * P, f"{xr.name}: REDC input {T / P / P:.1f} p^2"
+
+
+def run_xround(xr, F, A, B):
+    """Interprets a compiled round on plain residues; returns {dst: value}."""
+    S = {}
+
+    def get(code):
+        if code >= X_SCR:
+            return S[code]
+        if code >= X_SLOT_B:
+            return B[code - X_SLOT_B]
+        if code >= SLOT_A:
+            return A[code - SLOT_A]
+        return F[code]
+
+    for L in xr.lanes:
+        for dst, terms in L["pre"]:
+            if dst != NONE:
+                S[dst] = sum(k * get(src) for src, k in terms) % P
+    out = {}
+    for L in xr.lanes:
+        if L["dst"] == NONE:
+            continue
+        acc = sum(get(u) * get(v) for u, v in L["prod"]) + sum(k * get(src) for src, k in L["lin"])
+        out[L["dst"]] = acc % P
+    return out
+
+
+SCRATCH_CAP = {"FE": 96, "ML": 48}
+X_PROGRAMS = {  # name -> (program, scratch context)
+    "DBL": "ML", "ADD_POS": "ML", "ADD_NEG": "ML", "ADD_F1": "ML", "ADD_F2": "ML",
+    "SQR12": "ML", "LINE_PK": "ML", "LINE_FIX": "ML", "CYC_SQR": "FE", "MUL12": "FE", "CYC_SQR_X": "FE",
+}
+
+
+def compile_all():
+    return {name: [compile_round(r, f"{name}[{i}]", SCRATCH_CAP[ctx]) for i, r in enumerate(PROGRAMS[name])]
+            for name, ctx in X_PROGRAMS.items()}
+
+
+def run_xprogram(rounds, F, A=None, B=None):
+    """F: register dict (mutated), A/B: slot element lists; returns the D slot (dict e -> v)."""
+    A = A or [0] * 12
+    B = B or [0] * 12
+    D = {}
+    for xr in rounds:
+        out = run_xround(xr, F, A, B)
+        for dst, v in out.items():
+            if dst < 128:
+                F[dst] = v
+            else:
+                D[dst - 128] = v
+    return D
+
+
+def validate_x(seed=2):
+    """The compiled programs against the oracle (same cases as validate())."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from oracle import bn256_oracle as O
+
+    X = compile_all()
+    rng = random.Random(seed)
+    for trial in range(3):
+        Q = O.g2_mul(O.G2_GEN, rng.randrange(1, O.ORDER))
+        Hp = O.g1_mul(O.G1_GEN, rng.randrange(1, O.ORDER))
+        Rj = O.jac_mul(O.FP2_OPS, O.to_jac(O.FP2_OPS, Q), rng.randrange(2, 1000))
+        r = (Rj[0], Rj[1], Rj[2], O.f2_sqr(Rj[2]))
+        F = {i: rng.randrange(P) for i in range(NREGS)}
+        F[REG["ZERO"]] = 0
+        F[REG["ONE"]] = 1
+        F[REG["PX"]], F[REG["PY"]] = Hp
+
+        def put(G, n, v):
+            G[comp(n, "x")], G[comp(n, "y")] = v
+
+        def getf(G, n):
+            return (G[comp(n, "x")], G[comp(n, "y")])
+
+        for n, v in zip(("X", "Y", "Z", "T"), r):
+            put(F, n, v)
+        put(F, "QX", Q[0])
+        put(F, "QY", Q[1])
+        put(F, "NQY", O.f2_neg(Q[1]))
+        put(F, "R2", O.f2_sqr(Q[1]))
+        a, b, c, r_new = O._line_double(r, *Hp)
+        G = dict(F)
+        run_xprogram(X["DBL"], G)
+        assert [getf(G, n) for n in ("X", "Y", "Z", "T")] == list(r_new), "xDBL point"
+        assert [getf(G, n) for n in ("LA", "LB", "LC")] == [a, b, c], "xDBL line"
+        for prog, pq in (("ADD_POS", (Q[0], Q[1])), ("ADD_NEG", (Q[0], O.f2_neg(Q[1])))):
+            a, b, c, r_new = O._line_add(r, pq, *Hp, O.f2_sqr(pq[1]))
+            G = dict(F)
+            run_xprogram(X[prog], G)
+            assert [getf(G, n) for n in ("X", "Y", "Z", "T")] == list(r_new), "x" + prog
+            assert [getf(G, n) for n in ("LA", "LB", "LC")] == [a, b, c], "x" + prog + " line"
+        f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+        g = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+        flat = lambda v: [z for pair in v for z in pair]  # noqa: E731
+        unflat = lambda D: [(D[2 * k], D[2 * k + 1]) for k in range(6)]  # noqa: E731
+        cyc = O.f12_mul(O.f12_conj(f), O.f12_inv(f))
+        cyc = O.f12_mul(cyc, O.f12_frob2(cyc))
+        assert unflat(run_xprogram(X["SQR12"], dict(F), flat(f))) == O.f12_sqr(f), "xSQR12"
+        assert unflat(run_xprogram(X["CYC_SQR"], dict(F), flat(cyc))) == O.f12_sqr(cyc), "xCYC_SQR"
+        assert unflat(run_xprogram(X["CYC_SQR_X"], dict(F), flat(cyc))) == O.f12_sqr(cyc), "xCYC_SQR_X"
+        assert unflat(run_xprogram(X["MUL12"], dict(F), flat(f), flat(g))) == O.f12_mul(f, g), "xMUL12"
+        G = dict(F)
+        la, lb, lc = [(rng.randrange(P), rng.randrange(P)) for _ in range(3)]
+        for regs in (("LA", "LB", "LC", "LINE_PK"), ("FA", "FB", "FC", "LINE_FIX")):
+            put(G, regs[0], la)
+            put(G, regs[1], lb)
+            put(G, regs[2], lc)
+            want = O._mul_line(f, la, lb, lc)
+            assert unflat(run_xprogram(X[regs[3]], G, flat(f))) == want, "x" + regs[3]
+    return X
+
+
+# ------------------------------------------------------------------ per-call-site instances
+# Team LDS (bn256_pairing.h): 12 Fp12 slots of 12 elements, then the register
+# file F; operands become absolute team element indices (slot s element e ->
+# 12 s + e, register r -> 144 + r), so the executor needs no address selects.
+SLOTS = ["F", "A", "B", "C", "D", "E", "G", "H", "I", "J", "K", "L"]   # enum S_F.. (bn256_pairing.h)
+F_BASE = 12 * len(SLOTS)
+SCR_BASE = {"FE": F_BASE + 2, "ML": 12 * SLOTS.index("C")}
+
+
+def _pow_u_mul_instances(dst, sa):
+    return [("MUL12", ("J", "J", sa))] + [("MUL12", (dst, dst, m)) for m in (sa, "J", "K", "L")] + \
+        [("CYC_SQR_X", ("J", sa)), ("CYC_SQR_X", (dst, dst))]
+
+
+INSTANCES = sorted(set(
+    [("MUL12", b) for b in [("F", "B", "A"), ("F", "F", "A"), ("A", "A", "B"), ("H", "C", "H"), ("I", "E", "I"),
+                            ("K", "K", "H"), ("K", "K", "D"), ("J", "G", "D"), ("J", "J", "K"), ("K", "K", "C"),
+                            ("K", "J", "L"), ("J", "J", "A"), ("F", "K", "J"), ("L", "F", "K"), ("A", "K", "L"),
+                            ("F", "A", "B"), ("L", "A", "K"), ("F", "K", "L")]]
+    + _pow_u_mul_instances("C", "F") + _pow_u_mul_instances("D", "C") + _pow_u_mul_instances("E", "D")
+    + _pow_u_mul_instances("F", "A")
+    + [("CYC_SQR_X", b) for b in [("K", "I"), ("J", "J"), ("K", "K"), ("F", "A")]]
+    + [("SQR12", ("F", "F")), ("SQR12", ("F", "A")), ("LINE_PK", ("F", "F")), ("LINE_FIX", ("F", "F"))]
+    # tools/opcycles.hip
+    + [("CYC_SQR_X", ("A", "A")), ("SQR12", ("A", "A")), ("LINE_PK", ("A", "A"))]
+    + [(g, ()) for g in ("DBL", "ADD_POS", "ADD_NEG", "ADD_F1", "ADD_F2")]))
+
+
+def bind(xr, binding, ctx):
+    """Translates a compiled round to absolute team element indices."""
+    D, A, B = (list(binding) + [None, None, None])[:3]
+    if len(binding) == 2:
+        D, A = binding
+        B = A
+    sbase = SCR_BASE[ctx]
+
+    def src(code):
+        if code >= X_SCR:
+            return sbase + (code - X_SCR)
+        if code >= X_SLOT_B:
+            return 12 * SLOTS.index(B) + (code - X_SLOT_B)
+        if code >= SLOT_A:
+            return 12 * SLOTS.index(A) + (code - SLOT_A)
+        return F_BASE + code
+
+    def dst(code):
+        if code == NONE:
+            return NONE
+        if code >= SLOT_A:
+            return 12 * SLOTS.index(D) + (code - SLOT_A)
+        return F_BASE + code
+
+    lanes = []
+    for L in xr.lanes:
+        lanes.append({"pre": [(NONE if d == NONE else src(d), [(src(s), c) for s, c in t]) for d, t in L["pre"]],
+                      "prod": [(src(u), src(v)) for u, v in L["prod"]],
+                      "lin": [(src(s), c) for s, c in L["lin"]], "dst": dst(L["dst"])})
+    for L in lanes:
+        for v in [L["dst"]] + [d for d, _ in L["pre"]]:
+            assert v == NONE or v < F_BASE + NREGS, "index out of the team region"
+    out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name)
+    return out
+
+
+def run_bound(rounds, mem):
+    """Interprets bound rounds on a flat team memory (list of residues)."""
+    for xr in rounds:
+        for L in xr.lanes:
+            for d, terms in L["pre"]:
+                if d != NONE:
+                    mem[d] = sum(k * mem[s] for s, k in terms) % P
+        out = {}
+        for L in xr.lanes:
+            if L["dst"] != NONE:
+                out[L["dst"]] = (sum(mem[u] * mem[v] for u, v in L["prod"])
+                                 + sum(k * mem[s] for s, k in L["lin"])) % P
+        for d, v in out.items():
+            mem[d] = v
+
+
+def check_instances(X, seed=3):
+    """Every bound instance computes the same as the abstract program."""
+    rng = random.Random(seed)
+    for name, binding in INSTANCES:
+        ctx = X_PROGRAMS[name]
+        rounds = [bind(xr, binding, ctx) for xr in X[name]]
+        mem = [rng.randrange(P) for _ in range(F_BASE + NREGS)]
+        mem[F_BASE + REG["ZERO"]] = 0
+        mem[F_BASE + REG["ONE"]] = 1
+        F = {r: mem[F_BASE + r] for r in range(NREGS)}
+        A = B = None
+        if binding:
+            bd = list(binding) + ([binding[1]] if len(binding) == 2 else [])
+            A = mem[12 * SLOTS.index(bd[1]):12 * SLOTS.index(bd[1]) + 12]
+            B = mem[12 * SLOTS.index(bd[2]):12 * SLOTS.index(bd[2]) + 12]
+        want_D = run_xprogram(X[name], F, A, B)
+        run_bound(rounds, mem)
+        if binding:
+            d0 = 12 * SLOTS.index(binding[0])
+            assert all(mem[d0 + e] == v for e, v in want_D.items()), f"instance {name}{binding}"
+        else:
+            for r, v in F.items():
+                assert mem[F_BASE + r] == v, f"instance {name} reg {r}"
+
+
+def emit_x(X, path):
+    lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
+             "// Two-phase team programs executed by bn256_xprog.h (encoding: see there),",
+             "// one table per call-site instance (absolute team element indices).",
+             "#pragma once", "#include <stdint.h>", "namespace hg {",
+             "#define HG_P2N " + ", ".join("0x%08xu" % v for v in P2N),
+             "enum XProg { " + ", ".join(f"XP_{n}" for n in X_PROGRAMS) + " };",
+             "template <int PROG, int D = -1, int A = -1, int B = -1> struct XInst;"]
+    words = []
+    for name, binding in INSTANCES:
+        ctx = X_PROGRAMS[name]
+        calls = []
+        for xr in X[name]:
+            bx = bind(xr, binding, ctx)
+            off = len(words)
+            for t in range(16):
+                hv = bx.lane_halves(t)
+                words += [hv[2 * w] | (hv[2 * w + 1] << 16) for w in range(bx.words())]
+            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}>(T, kXTab + {off});")
+        args = ", ".join(f"S_{b}" for b in binding)
+        targs = f"XP_{name}" + (", " + args if args else "")
+        lines.append(f"template <> struct XInst<{targs}> {{ HG_DEV static void run(const Team& T) {{ "
+                     + " ".join(calls) + " } };")
+    lines.insert(9, f"__constant__ static const uint32_t kXTab[{len(words)}] = {{")
+    tab = []
+    for i in range(0, len(words), 12):
+        tab.append("  " + ", ".join("0x%08xu" % w for w in words[i:i + 12]) + ",")
+    tab.append("};")
+    lines[10:10] = tab
+    lines.append("}  // namespace hg")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return len(words)
+
+
 # ------------------------------------------------------------------ emit
 def emit(path):
     lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
@@ -394,6 +915,8 @@ def emit(path):
     all_lanes = []
     rounds = {}
     for name, prog in PROGRAMS.items():
+        if name not in LEGACY:
+            continue
         rounds[name] = []
         for r in prog:
             nslot = max(len(l.slots) for l in r)
@@ -431,6 +954,12 @@ def emit(path):
 
 if __name__ == "__main__":
     validate()
-    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "handel_amd", "csrc", "bn256_g2sched.h")
-    emit(out)
-    print("validated and wrote", os.path.normpath(out))
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "handel_amd", "csrc")
+    emit(os.path.join(csrc, "bn256_g2sched.h"))
+    Xp = validate_x()
+    check_instances(Xp)
+    nwords = emit_x(Xp, os.path.join(csrc, "bn256_xtab.h"))
+    print(len(INSTANCES), "instances,", nwords * 4, "table bytes")
+    for name, rounds in Xp.items():
+        print(name, [(r.nv, r.nt, r.np, r.nl, r.words()) for r in rounds])
+    print("validated and wrote bn256_g2sched.h, bn256_xtab.h")

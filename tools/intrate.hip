@@ -70,6 +70,38 @@ __global__ __launch_bounds__(256) void k_add(uint64_t* out, uint32_t seed) {
     if (s == 0x12345) out[0] = s;                                                       \
   }
 K32(k_mul_lo, "v_mul_lo_u32")
+K32(k_mul_hi, "v_mul_hi_u32")
+K32(k_and, "v_and_b32")
+K32(k_sub, "v_sub_u32")
+
+// 64-bit-result ops: 8 independent 64-bit chains
+#define K64(NAME, BODY)                                                                        \
+  __global__ __launch_bounds__(256) void NAME(uint64_t* out, uint32_t seed) {                  \
+    uint32_t a = seed ^ threadIdx.x;                                                           \
+    uint64_t c0 = a, c1 = a + 1, c2 = a + 2, c3 = a + 3, c4 = a + 4, c5 = a + 5, c6 = a + 6,    \
+             c7 = a + 7;                                                                       \
+    for (int it = 0; it < ITERS; it++) {                                                       \
+      asm volatile(BODY : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), \
+                   "+v"(c7) : "v"(a));                                                         \
+    }                                                                                          \
+    uint64_t s = c0 ^ c1 ^ c2 ^ c3 ^ c4 ^ c5 ^ c6 ^ c7;                                        \
+    if (s == 0x12345) out[0] = s;                                                              \
+  }
+#define B8(I) I(0) I(1) I(2) I(3) I(4) I(5) I(6) I(7)
+#define LSHLADD(n) "v_lshl_add_u64 %" #n ", %" #n ", 1, %" #n "\n\t"
+#define LSHR64(n) "v_lshrrev_b64 %" #n ", 3, %" #n "\n\t"
+#define MADU24(n) "v_mad_u32_u24 %" #n ", %8, %8, %" #n "\n\t"
+K64(k_lshl_add_u64, B8(LSHLADD))
+K64(k_lshr_b64, B8(LSHR64))
+__global__ __launch_bounds__(256) void k_mad_u24(uint64_t* out, uint32_t seed) {
+  uint32_t a = seed ^ threadIdx.x, b = seed * 2654435761u + blockIdx.x;
+  uint32_t c0 = a, c1 = b, c2 = a + 1, c3 = b + 1, c4 = a + 2, c5 = b + 2, c6 = a + 3, c7 = b + 3;
+  for (int it = 0; it < ITERS; it++)
+    asm volatile(B8(MADU24) : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7)
+                 : "v"(a));
+  uint64_t s = c0 ^ c1 ^ c2 ^ c3 ^ c4 ^ c5 ^ c6 ^ c7;
+  if (s == 0x12345) out[0] = s;
+}
 K32(k_mul_u24, "v_mul_u32_u24")
 K32(k_lshl, "v_lshlrev_b32")
 
@@ -103,6 +135,12 @@ int main() {
     printf("{\"op\": \"v_mul_lo_u32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_mul_lo, blocks, d));
     printf("{\"op\": \"v_mul_u32_u24\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_mul_u24, blocks, d));
     printf("{\"op\": \"v_lshlrev_b32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_lshl, blocks, d));
+    printf("{\"op\": \"v_mul_hi_u32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_mul_hi, blocks, d));
+    printf("{\"op\": \"v_and_b32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_and, blocks, d));
+    printf("{\"op\": \"v_sub_u32\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_sub, blocks, d));
+    printf("{\"op\": \"v_lshl_add_u64\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_lshl_add_u64, blocks, d));
+    printf("{\"op\": \"v_lshrrev_b64\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_lshr_b64, blocks, d));
+    printf("{\"op\": \"v_mad_u32_u24\", \"waves_per_simd\": %d, \"tops\": %.3f}\n", per_cu, run(k_mad_u24, blocks, d));
   }
   (void)hipFree(d);
   return 0;
