@@ -35,8 +35,9 @@ __global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* 
   C.hy = P.y;
   fp_zero(C.sx);
   fp_zero(C.sy);
-  team_miller_check(T, F, C, tab, false);
-  team_final_exp(T, F);  // f == 1 when either input is infinity, and 1^e == 1
+  XStream S = x_stream();
+  team_miller_check(T, F, C, tab, false, S, final_exp_hint());
+  team_final_exp(T, F, S);  // f == 1 when either input is infinity, and 1^e == 1
   // GT.Marshal order: coefficients 5,3,1,4,2,0, each as (x, y)
   if (valid && T.active) {
     const int pos[6] = {5, 2, 4, 1, 3, 0};  // position of coefficient k in the marshal
@@ -83,18 +84,19 @@ __global__ __launch_bounds__(64) void k_fp12_op(int op, const uint8_t* a, const 
   // applications feed the result back as the input)
   int reps = (op >> 8) > 0 ? (op >> 8) : 1;
   op &= 255;
+  XStream S = x_stream();
   for (int r = 0; r < reps; r++) {
     if (r > 0) t12_copy(T, S_A, S_F);
     switch (op) {  // kernel-uniform
-      case 0: x_mul12<S_F, S_A, S_B>(T); break;
-      case 1: x_sqr12<S_F, S_A>(T); break;
-      case 2: x_cyc_sqr<S_F, S_A>(T); break;
+      case 0: x_mul12<S_F, S_A, S_B>(T, S, xh_none()); break;
+      case 1: x_sqr12<S_F, S_A>(T, S, xh_none()); break;
+      case 2: x_cyc_sqr<S_F, S_A>(T, S, xh_none()); break;
       case 3: t12_frob(T, S_F, S_A); break;
       case 4: t12_frob2(T, S_F, S_A); break;
-      case 5: t12_inv_x<S_F, S_A, S_K, S_L>(T); break;
+      case 5: t12_inv_x<S_F, S_A, S_K, S_L>(T, S, xh_none()); break;
       case 6: t12_conj(T, S_F, S_A); break;
-      case 7: t12_pow_u_x<S_F, S_A>(T); break;
-      case 8: t12_copy(T, S_F, S_A); team_final_exp(T, F); break;
+      case 7: t12_pow_u_x<S_F, S_A>(T, S, xh_none()); break;
+      case 8: t12_copy(T, S_F, S_A); team_final_exp(T, F, S); break;
       case 9: t12_sqr_fast(T, S_F, S_A); break;
       case 10: t12_cyc_sqr(T, S_F, S_A); break;
       default: t12_copy(T, S_F, S_A); break;

@@ -31,51 +31,54 @@ extern __device__ uint64_t g_diag[4096 * 16];
 static constexpr int kTeamWords = kSlots * kFp12Words + kG2Regs * 10;
 static constexpr int kTeamsPerBlock = 4;
 
-// the pairing's final exponentiation (x/crypto optate.go finalExponentiation)
-HG_DEV void team_final_exp(const Team& T, uint32_t* F) {
+// the pairing's final exponentiation (x/crypto optate.go finalExponentiation);
+// every program call names the program that follows it (table prefetch, bn256_xprog.h)
+HG_DEV void team_final_exp(const Team& T, uint32_t* F, XStream& S) {
   DIAG_T0();
-  t12_inv_x<S_A, S_F, S_K, S_L>(T);  // A = f^-1
+  t12_inv_x<S_A, S_F, S_K, S_L>(T, S, xh<IMul12<S_F, S_B, S_A>>());  // A = f^-1
   DIAG_ADD(5);
-  t12_conj(T, S_B, S_F);           // B = conj(f)
-  x_mul12<S_F, S_B, S_A>(T);       // t1 = f^(p^6 - 1)
+  t12_conj(T, S_B, S_F);                                        // B = conj(f)
+  x_mul12<S_F, S_B, S_A>(T, S, xh<IMul12<S_F, S_F, S_A>>());   // t1 = f^(p^6 - 1)
   t12_frob2(T, S_A, S_F);
-  x_mul12<S_F, S_F, S_A>(T);       // t1 = t1^(p^2 + 1)
-  t12_frob(T, S_A, S_F);           // fp
-  t12_frob2(T, S_B, S_F);          // fp2
-  x_mul12<S_A, S_A, S_B>(T);
-  t12_frob(T, S_B, S_B);           // fp3
-  x_mul12<S_A, S_A, S_B>(T);       // y0 = fp * fp2 * fp3
+  x_mul12<S_F, S_F, S_A>(T, S, xh<IMul12<S_A, S_A, S_B>>());   // t1 = t1^(p^2 + 1)
+  t12_frob(T, S_A, S_F);                                        // fp
+  t12_frob2(T, S_B, S_F);                                       // fp2
+  x_mul12<S_A, S_A, S_B>(T, S, xh<IMul12<S_A, S_A, S_B>>());
+  t12_frob(T, S_B, S_B);                                        // fp3
+  x_mul12<S_A, S_A, S_B>(T, S, xh<ICyc<S_J, S_F>>());          // y0 = fp * fp2 * fp3
   DIAG_ADD(6);
-  t12_pow_u_x<S_C, S_F>(T);       // fu
-  t12_pow_u_x<S_D, S_C>(T);       // fu2
-  t12_pow_u_x<S_E, S_D>(T);       // fu3
+  t12_pow_u_x<S_C, S_F>(T, S, xh<ICyc<S_J, S_C>>());           // fu
+  t12_pow_u_x<S_D, S_C>(T, S, xh<ICyc<S_J, S_D>>());           // fu2
+  t12_pow_u_x<S_E, S_D>(T, S, xh<IMul12<S_H, S_C, S_H>>());    // fu3
   DIAG_ADD(7);
   t12_frob(T, S_G, S_C);
-  t12_conj(T, S_G, S_G);           // y3 = conj(frob(fu))
+  t12_conj(T, S_G, S_G);                                        // y3 = conj(frob(fu))
   t12_frob(T, S_H, S_D);
-  x_mul12<S_H, S_C, S_H>(T);
-  t12_conj(T, S_H, S_H);           // y4 = conj(fu * frob(fu2))
-  t12_frob2(T, S_C, S_D);          // y2 = frob2(fu2)
-  t12_conj(T, S_D, S_D);           // y5 = conj(fu2)
+  x_mul12<S_H, S_C, S_H>(T, S, xh<IMul12<S_I, S_E, S_I>>());
+  t12_conj(T, S_H, S_H);                                        // y4 = conj(fu * frob(fu2))
+  t12_frob2(T, S_C, S_D);                                       // y2 = frob2(fu2)
+  t12_conj(T, S_D, S_D);                                        // y5 = conj(fu2)
   t12_frob(T, S_I, S_E);
-  x_mul12<S_I, S_E, S_I>(T);
-  t12_conj(T, S_I, S_I);           // y6 = conj(fu3 * frob(fu3))
-  x_cyc_sqr<S_K, S_I>(T);
-  x_mul12<S_K, S_K, S_H>(T);
-  x_mul12<S_K, S_K, S_D>(T);       // t0 = y6^2 y4 y5
-  x_mul12<S_J, S_G, S_D>(T);
-  x_mul12<S_J, S_J, S_K>(T);       // t1 = y3 y5 t0
-  x_mul12<S_K, S_K, S_C>(T);       // t0 = t0 y2
-  x_cyc_sqr<S_J, S_J>(T);
-  x_mul12<S_J, S_J, S_K>(T);
-  x_cyc_sqr<S_J, S_J>(T);            // t1 = (t1^2 t0)^2
-  t12_conj(T, S_L, S_F);           // y1 = conj(t1_easy)
-  x_mul12<S_K, S_J, S_L>(T);       // t0 = t1 y1
-  x_mul12<S_J, S_J, S_A>(T);       // t1 = t1 y0
-  x_cyc_sqr<S_K, S_K>(T);
-  x_mul12<S_F, S_K, S_J>(T);       // result
+  x_mul12<S_I, S_E, S_I>(T, S, xh<ICyc<S_K, S_I>>());
+  t12_conj(T, S_I, S_I);                                        // y6 = conj(fu3 * frob(fu3))
+  x_cyc_sqr<S_K, S_I>(T, S, xh<IMul12<S_K, S_K, S_H>>());
+  x_mul12<S_K, S_K, S_H>(T, S, xh<IMul12<S_K, S_K, S_D>>());
+  x_mul12<S_K, S_K, S_D>(T, S, xh<IMul12<S_J, S_G, S_D>>());   // t0 = y6^2 y4 y5
+  x_mul12<S_J, S_G, S_D>(T, S, xh<IMul12<S_J, S_J, S_K>>());
+  x_mul12<S_J, S_J, S_K>(T, S, xh<IMul12<S_K, S_K, S_C>>());   // t1 = y3 y5 t0
+  x_mul12<S_K, S_K, S_C>(T, S, xh<ICyc<S_J, S_J>>());          // t0 = t0 y2
+  x_cyc_sqr<S_J, S_J>(T, S, xh<IMul12<S_J, S_J, S_K>>());
+  x_mul12<S_J, S_J, S_K>(T, S, xh<ICyc<S_J, S_J>>());
+  x_cyc_sqr<S_J, S_J>(T, S, xh<IMul12<S_K, S_J, S_L>>());      // t1 = (t1^2 t0)^2
+  t12_conj(T, S_L, S_F);                                        // y1 = conj(t1_easy)
+  x_mul12<S_K, S_J, S_L>(T, S, xh<IMul12<S_J, S_J, S_A>>());   // t0 = t1 y1
+  x_mul12<S_J, S_J, S_A>(T, S, xh<ICyc<S_K, S_K>>());          // t1 = t1 y0
+  x_cyc_sqr<S_K, S_K>(T, S, xh<IMul12<S_F, S_K, S_J>>());
+  x_mul12<S_F, S_K, S_J>(T, S, xh_none());                      // result
   DIAG_ADD(6);
 }
+// the first program team_final_exp runs (t12_inv_x<S_A, S_F, S_K, S_L>)
+HG_DEV constexpr XHint final_exp_hint() { return xh<IMul12<S_L, S_F, S_K>>(); }
 
 // Per-check inputs of the team Miller loop.
 struct CheckCtx {
@@ -163,17 +166,21 @@ HG_DEV void unit_lines(const Team& T, uint32_t* F, const CheckCtx& C, bool has_f
   team_sync();
 }
 
-// f *= pk line (LA, LB, LC) and, when has_fixed, the G2Base line (FA, FB, FC)
-HG_DEV void apply_lines(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed) {
+// f *= pk line (LA, LB, LC) and, when has_fixed, the G2Base line (FA, FB, FC);
+// next: the program that runs after the lines
+HG_DEV void apply_lines(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed, XStream& S, XHint next) {
   unit_lines(T, F, C, has_fixed);
-  x_line_pk<S_F, S_F>(T);
-  if (has_fixed) x_line_fix<S_F, S_F>(T);
+  x_line_pk<S_F, S_F>(T, S, has_fixed ? xh<ILineFix<S_F, S_F>>() : next);
+  if (has_fixed) x_line_fix<S_F, S_F>(T, S, next);
 }
 
 // f = Miller(pk at H) * Miller(G2Base at -sig) (x/crypto optate.go miller, with
 // the two loops sharing their squarings); the G2 steps run as team programs.
-HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, const LineCoef* tab, bool has_fixed) {
+// after: the program that runs after the loop.
+HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, const LineCoef* tab, bool has_fixed,
+                              XStream& S, XHint after) {
   const int8_t naf[kNafLen] = HG_NAF;
+  constexpr XHint kLinePk = xh<ILinePk<S_F, S_F>>();
   t12_set_one(T, S_F);
   g2_regs_init(T, F, C);
   int s = 0;
@@ -181,29 +188,30 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   for (int i = kNafLen - 1; i > 0; i--) {
     load_fixed_line(T, F, tab, s++);
     DIAG_ADD(0);
-    x_g2<XP_DBL>(T);
+    x_g2<XP_DBL>(T, S, i != kNafLen - 1 ? xh<ISqr12<S_F, S_F>>() : kLinePk);
     DIAG_ADD(1);
-    if (i != kNafLen - 1) x_sqr12<S_F, S_F>(T);
+    if (i != kNafLen - 1) x_sqr12<S_F, S_F>(T, S, kLinePk);
     DIAG_ADD(2);
-    apply_lines(T, F, C, has_fixed);
+    const int d = naf[i - 1];
+    const XHint step = i > 1 ? xh<IG2<XP_DBL>>() : xh<IG2<XP_ADD_F1>>();  // after this digit
+    apply_lines(T, F, C, has_fixed, S, d > 0 ? xh<IG2<XP_ADD_POS>>() : d < 0 ? xh<IG2<XP_ADD_NEG>>() : step);
     DIAG_ADD(3);
-    int d = naf[i - 1];
     if (d != 0) {
       load_fixed_line(T, F, tab, s++);
       DIAG_ADD(0);
-      if (d > 0) x_g2<XP_ADD_POS>(T);
-      else x_g2<XP_ADD_NEG>(T);
+      if (d > 0) x_g2<XP_ADD_POS>(T, S, kLinePk);
+      else x_g2<XP_ADD_NEG>(T, S, kLinePk);
       DIAG_ADD(4);
-      apply_lines(T, F, C, has_fixed);
+      apply_lines(T, F, C, has_fixed, S, step);
       DIAG_ADD(3);
     }
   }
   load_fixed_line(T, F, tab, s++);
-  x_g2<XP_ADD_F1>(T);
-  apply_lines(T, F, C, has_fixed);
+  x_g2<XP_ADD_F1>(T, S, kLinePk);
+  apply_lines(T, F, C, has_fixed, S, xh<IG2<XP_ADD_F2>>());
   load_fixed_line(T, F, tab, s++);
-  x_g2<XP_ADD_F2>(T);
-  apply_lines(T, F, C, has_fixed);
+  x_g2<XP_ADD_F2>(T, S, kLinePk);
+  apply_lines(T, F, C, has_fixed, S, after);
 }
 
 HG_DEV uint32_t* team_regs(const Team& T) { return T.base + kSlots * kFp12Words; }

@@ -45,11 +45,12 @@ __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const L
   __syncthreads();
   uint64_t diag_start = __builtin_amdgcn_s_memtime();
 #endif
-  team_miller_check(T, F, C, tab, true);
+  XStream S = x_stream();
+  team_miller_check(T, F, C, tab, true, S, final_exp_hint());
 #ifdef HG_DIAG
   uint64_t diag_mid = __builtin_amdgcn_s_memtime();
 #endif
-  team_final_exp(T, F);
+  team_final_exp(T, F, S);
   bool ok = t12_is_one(T, S_F);
   if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
 #ifdef HG_DIAG

@@ -30,8 +30,18 @@
 namespace hg {
 
 struct Team;
-template <int NV, int NT, int NP, int NL, int W>
-HG_DEV void x_round(const Team& T, const uint32_t* tab);
+// Table prefetch (software pipelining of the per-lane round tables): every
+// round starts by issuing the load of the NEXT round's words, so the ~600-cycle
+// L1/L2 latency of the table read overlaps the current round's arithmetic
+// instead of stalling its start. The stream remembers which round's words it
+// holds; a round whose words are not there (no or a wrong hint) fetches them
+// itself, so hints only affect speed, never results.
+struct XHint {
+  int off, w;  // table offset and per-lane stride of the round to prefetch (off < 0: none)
+};
+struct XStream;
+template <int NV, int NT, int NP, int NL, int W, int OFF>
+HG_DEV void x_round(const Team& T, XStream& S, XHint nxt);
 
 }  // namespace hg
 
@@ -40,6 +50,27 @@ HG_DEV void x_round(const Team& T, const uint32_t* tab);
 namespace hg {
 
 static constexpr uint32_t kP2N[10] = {HG_P2N};
+
+struct XStream {
+  uint32_t w[kXFetchWords];
+  int off;  // table offset the words belong to (-1: none)
+};
+HG_DEV void x_fetch(const Team& T, XStream& S, XHint h) {
+  const uint32_t* src = kXTab + h.off + T.tl * h.w;
+#pragma unroll
+  for (int i = 0; i < kXFetchWords; i++) S.w[i] = src[i];
+  S.off = h.off;
+}
+HG_DEV XStream x_stream() {
+  XStream S;
+  S.off = -1;
+  return S;
+}
+template <class I>
+HG_DEV constexpr XHint xh() {
+  return XHint{I::kOff, I::kW};
+}
+HG_DEV constexpr XHint xh_none() { return XHint{-1, 0}; }
 
 template <int... I, typename Fn>
 HG_DEV void x_static_for(std::integer_sequence<int, I...>, Fn&& f) {
@@ -95,11 +126,12 @@ HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t 
 
 // One round. Table layout per lane (16-bit entries): NV x (dst, NT x term),
 // NP x (u, v), NL x term, dst; padded to W dwords.
-template <int NV, int NT, int NP, int NL, int W>
-HG_DEV void x_round(const Team& T, const uint32_t* tab) {
+template <int NV, int NT, int NP, int NL, int W, int OFF>
+HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
+  if (S.off != OFF) x_fetch(T, S, XHint{OFF, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
-  const uint32_t* my = tab + T.tl * W;
-  x_for<W>([&](auto i) { w[i] = my[i]; });
+  x_for<W>([&](auto i) { w[i] = S.w[i]; });
+  if (nxt.off >= 0) x_fetch(T, S, nxt);
   if constexpr (NV > 0) {
     x_for<NV>([&](auto v) {
       constexpr int base = v * (1 + NT);
@@ -139,57 +171,80 @@ HG_DEV void x_round(const Team& T, const uint32_t* tab) {
 }
 
 // ------------------------------------------------------------------ call-site wrappers
+// Each takes the stream and a hint naming the program that runs next.
+template <int D, int A, int B>
+using IMul12 = XInst<XP_MUL12, D, A, B>;
+template <int D, int A>
+using ICyc = XInst<XP_CYC_SQR_X, D, A>;
+template <int D, int A>
+using ISqr12 = XInst<XP_SQR12, D, A>;
+template <int D, int A>
+using ILinePk = XInst<XP_LINE_PK, D, A>;
+template <int D, int A>
+using ILineFix = XInst<XP_LINE_FIX, D, A>;
+template <int PROG>
+using IG2 = XInst<PROG>;
+
 // dst = a * b (Fp12)
 template <int D, int A, int B>
-HG_DEV void x_mul12(const Team& T) { XInst<XP_MUL12, D, A, B>::run(T); }
+HG_DEV void x_mul12(const Team& T, XStream& S, XHint h) { IMul12<D, A, B>::run(T, S, h); }
 // dst = a^2 for a in the cyclotomic subgroup (Granger-Scott)
 template <int D, int A>
-HG_DEV void x_cyc_sqr(const Team& T) { XInst<XP_CYC_SQR_X, D, A>::run(T); }
+HG_DEV void x_cyc_sqr(const Team& T, XStream& S, XHint h) { ICyc<D, A>::run(T, S, h); }
 // dst = a^2 (Miller loop)
 template <int D, int A>
-HG_DEV void x_sqr12(const Team& T) { XInst<XP_SQR12, D, A>::run(T); }
+HG_DEV void x_sqr12(const Team& T, XStream& S, XHint h) { ISqr12<D, A>::run(T, S, h); }
 // dst = a * (LC + LB w + LA w^3) / a * (FC + FB w + FA w^3): the pk / G2Base lines
 template <int D, int A>
-HG_DEV void x_line_pk(const Team& T) { XInst<XP_LINE_PK, D, A>::run(T); }
+HG_DEV void x_line_pk(const Team& T, XStream& S, XHint h) { ILinePk<D, A>::run(T, S, h); }
 template <int D, int A>
-HG_DEV void x_line_fix(const Team& T) { XInst<XP_LINE_FIX, D, A>::run(T); }
+HG_DEV void x_line_fix(const Team& T, XStream& S, XHint h) { ILineFix<D, A>::run(T, S, h); }
 // G2 Miller-loop steps on the register file (x/crypto lineFunctionDouble / Add)
 template <int PROG>
-HG_DEV void x_g2(const Team& T) { XInst<PROG>::run(T); }
+HG_DEV void x_g2(const Team& T, XStream& S, XHint h) { IG2<PROG>::run(T, S, h); }
 
 
 __constant__ static const int8_t kUNaf3X[kUNaf3Len] = HG_U_NAF3;
 
+// the program that multiplies by digit d (d != 0) in t12_pow_u_x
+template <int D, int SA>
+HG_DEV XHint pow_u_mul_hint(int d) {
+  return d == 1 ? xh<IMul12<D, D, SA>>() : d == 3 ? xh<IMul12<D, D, S_J>>()
+       : d == -1 ? xh<IMul12<D, D, S_K>>() : xh<IMul12<D, D, S_L>>();
+}
+
 // dst = a^u (x/crypto gfP12.Exp(t, u)) for a in the cyclotomic subgroup, where
 // a^-1 = conj(a): width-3 signed digits of u (62 cyclotomic squarings and 16
 // multiplications instead of 62 + 29). Scratch slots: J = a^3, K = a^-1,
-// L = a^-3 (dst, SA not among them).
+// L = a^-3 (dst, SA not among them). h: the program that runs after it.
 template <int D, int SA>
-HG_DEV void t12_pow_u_x(const Team& T) {
+HG_DEV void t12_pow_u_x(const Team& T, XStream& S, XHint h) {
   static_assert(D != S_J && D != S_K && D != S_L && SA != S_J && SA != S_K && SA != S_L, "scratch slots");
   static_assert(HG_U_NAF3_TOP == 3, "top digit of the width-3 NAF of u");
-  x_cyc_sqr<S_J, SA>(T);
-  x_mul12<S_J, S_J, SA>(T);  // a^3
+  x_cyc_sqr<S_J, SA>(T, S, xh<IMul12<S_J, S_J, SA>>());
+  x_mul12<S_J, S_J, SA>(T, S, xh<ICyc<D, D>>());  // a^3
   t12_conj(T, S_K, SA);      // a^-1
   t12_conj(T, S_L, S_J);     // a^-3
   t12_copy(T, D, S_J);
   for (int i = kUNaf3Len - 2; i >= 0; i--) {
-    x_cyc_sqr<D, D>(T);
     const int d = kUNaf3X[i];  // wave-uniform
-    if (d == 1) x_mul12<D, D, SA>(T);
-    else if (d == 3) x_mul12<D, D, S_J>(T);
-    else if (d == -1) x_mul12<D, D, S_K>(T);
-    else if (d == -3) x_mul12<D, D, S_L>(T);
+    // after this digit: the next squaring, or the caller's next program
+    const XHint after = i > 0 ? xh<ICyc<D, D>>() : h;
+    x_cyc_sqr<D, D>(T, S, d != 0 ? pow_u_mul_hint<D, SA>(d) : after);
+    if (d == 1) x_mul12<D, D, SA>(T, S, after);
+    else if (d == 3) x_mul12<D, D, S_J>(T, S, after);
+    else if (d == -1) x_mul12<D, D, S_K>(T, S, after);
+    else if (d == -3) x_mul12<D, D, S_L>(T, S, after);
   }
 }
 
 // dst = a^-1 (x/crypto gfP12.Invert) with scratch slots S1, S2
 template <int DST, int SA, int S1, int S2>
-HG_DEV void t12_inv_x(const Team& T) {
-  t12_conj(T, S1, SA);          // S1 = conj(a)
-  x_mul12<S2, SA, S1>(T);       // S2 = a conj(a) = N (even coefficients only)
-  t12_inv_norm(T, S2);          // S2 = N^-1
-  x_mul12<DST, S1, S2>(T);      // conj(a) / N
+HG_DEV void t12_inv_x(const Team& T, XStream& S, XHint h) {
+  t12_conj(T, S1, SA);                                       // S1 = conj(a)
+  x_mul12<S2, SA, S1>(T, S, xh<IMul12<DST, S1, S2>>());      // S2 = a conj(a) = N (even coefficients only)
+  t12_inv_norm(T, S2);                                       // S2 = N^-1
+  x_mul12<DST, S1, S2>(T, S, h);                             // conj(a) / N
 }
 
 }  // namespace hg

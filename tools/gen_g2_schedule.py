@@ -669,6 +669,7 @@ def run_xround(xr, F, A, B):
     return out
 
 
+X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
 SCRATCH_CAP = {"FE": 96, "ML": 48}
 X_PROGRAMS = {  # name -> (program, scratch context)
     "DBL": "ML", "ADD_POS": "ML", "ADD_NEG": "ML", "ADD_F1": "ML", "ADD_F2": "ML",
@@ -869,22 +870,31 @@ def emit_x(X, path):
              "#pragma once", "#include <stdint.h>", "namespace hg {",
              "#define HG_P2N " + ", ".join("0x%08xu" % v for v in P2N),
              "enum XProg { " + ", ".join(f"XP_{n}" for n in X_PROGRAMS) + " };",
+             f"static constexpr int kXFetchWords = {X_FETCH_WORDS};",
              "template <int PROG, int D = -1, int A = -1, int B = -1> struct XInst;"]
     words = []
     for name, binding in INSTANCES:
         ctx = X_PROGRAMS[name]
-        calls = []
+        rounds = []
         for xr in X[name]:
             bx = bind(xr, binding, ctx)
             off = len(words)
             for t in range(16):
                 hv = bx.lane_halves(t)
                 words += [hv[2 * w] | (hv[2 * w + 1] << 16) for w in range(bx.words())]
-            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}>(T, kXTab + {off});")
+            assert bx.words() <= X_FETCH_WORDS, f"{name}: round wider than the prefetch"
+            rounds.append((bx, off))
+        calls = []
+        for i, (bx, off) in enumerate(rounds):
+            # each round prefetches the next round's words (the last one: the caller's hint)
+            nxt = f"XHint{{{rounds[i + 1][1]}, {rounds[i + 1][0].words()}}}" if i + 1 < len(rounds) else "h"
+            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {off}>(T, S, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
-        lines.append(f"template <> struct XInst<{targs}> {{ HG_DEV static void run(const Team& T) {{ "
+        lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
+                     f"kW = {rounds[0][0].words()}; HG_DEV static void run(const Team& T, XStream& S, XHint h) {{ "
                      + " ".join(calls) + " } };")
+    words += [0] * X_FETCH_WORDS  # a prefetch reads X_FETCH_WORDS words from any lane's block
     lines.insert(9, f"__constant__ static const uint32_t kXTab[{len(words)}] = {{")
     tab = []
     for i in range(0, len(words), 12):

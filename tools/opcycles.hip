@@ -44,6 +44,7 @@ __global__ __launch_bounds__(64) void k_op(uint32_t seed, uint32_t* sink) {
     st_fp(F + R_ONE * 10, o);
   }
   __syncthreads();
+  XStream S = x_stream();  // each repetition prefetches the next one's table words
   uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int r = 0; r < REPS; r++) {
     if constexpr (OP == 0) t12_mul(T, S_A, S_A, S_B);
@@ -55,12 +56,12 @@ __global__ __launch_bounds__(64) void k_op(uint32_t seed, uint32_t* sink) {
     if constexpr (OP == 6) t12_conj(T, S_A, S_A);
     if constexpr (OP == 7) g2_program(T, F, kProgDBL);
     if constexpr (OP == 8) g2_program(T, F, kProgADD_POS);
-    if constexpr (OP == 10) x_cyc_sqr<S_A, S_A>(T);
-    if constexpr (OP == 11) x_mul12<S_A, S_A, S_B>(T);
-    if constexpr (OP == 12) x_sqr12<S_A, S_A>(T);
-    if constexpr (OP == 13) x_line_pk<S_A, S_A>(T);
-    if constexpr (OP == 14) x_g2<XP_DBL>(T);
-    if constexpr (OP == 15) x_g2<XP_ADD_POS>(T);
+    if constexpr (OP == 10) x_cyc_sqr<S_A, S_A>(T, S, xh<ICyc<S_A, S_A>>());
+    if constexpr (OP == 11) x_mul12<S_A, S_A, S_B>(T, S, xh<IMul12<S_A, S_A, S_B>>());
+    if constexpr (OP == 12) x_sqr12<S_A, S_A>(T, S, xh<ISqr12<S_A, S_A>>());
+    if constexpr (OP == 13) x_line_pk<S_A, S_A>(T, S, xh<ILinePk<S_A, S_A>>());
+    if constexpr (OP == 14) x_g2<XP_DBL>(T, S, xh<IG2<XP_DBL>>());
+    if constexpr (OP == 15) x_g2<XP_ADD_POS>(T, S, xh<IG2<XP_ADD_POS>>());
     if constexpr (OP == 9) {
       Fp v;
       ld_fp(v, slot(T, S_A) + T.e * 10);
