@@ -91,7 +91,7 @@ def pmc_traffic():
         vals = {}
         with open(path) as f:
             for row in csv.DictReader(f):
-                if row["kernel"] == "hg::k_verify":
+                if "k_verify" in row["kernel"]:
                     vals[row["counter"]] = float(row["avg"])
         if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
             return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(path, ROOT)

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "bn256_constants.h"
+#include "bn256_inv.h"
 
 #define HG_DEV __device__ __forceinline__
 
@@ -207,21 +208,6 @@ HG_DEV void fp_norm(Fp& r, const Fp& a) {
   fp_csub(r, x);
 }
 
-// a^(p-2)
-HG_DEV void fp_inv(Fp& r, const Fp& a) {
-  const uint32_t e[8] = {HG_P32};
-  Fp acc;
-  fp_one(acc);
-  for (int i = 7; i >= 0; i--) {
-    uint32_t ei = (i == 0) ? e[0] - 2u : e[i];
-    for (int bit = 31; bit >= 0; bit--) {
-      fp_sqr(acc, acc);
-      if ((ei >> bit) & 1) fp_mul(acc, acc, a);
-    }
-  }
-  r = acc;
-}
-
 // ---------------------------------------------------------------- conversions
 // 8 LE 32-bit words (a plain integer < 2^256) -> 10 x 26-bit limbs (no reduction)
 HG_DEV void words_to_limbs(Fp& r, const uint32_t* w) {
@@ -255,6 +241,19 @@ HG_DEV void fp_from_mont(Fp& r, const Fp& a) {
   fp_zero(one);
   one.l[0] = 1;
   fp_mul(r, a, one);
+}
+// a^-1 for canonical a (0 -> 0): the plain integer inverse of the Montgomery
+// representative aR (Bernstein-Yang, bn256_inv.h), times R^3 by one Montgomery
+// product: (aR)^-1 R^3 / R = a^-1 R. Replaces the a^(p-2) chain of x/crypto's
+// gfP.Invert with an equal result.
+HG_DEV void fp_inv(Fp& r, const Fp& a) {
+  uint32_t w[8];
+  limbs_to_words(w, a);
+  inv::inv_words(w);
+  Fp x;
+  words_to_limbs(x, w);
+  const Fp r3 = {{HG_R3}};
+  fp_mul(r, x, r3);
 }
 // big-endian 32 bytes -> LE words; returns true when the value is >= p
 HG_DEV bool be_to_words(uint32_t* w, const uint8_t* b) {
