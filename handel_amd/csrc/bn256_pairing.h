@@ -89,7 +89,7 @@ struct CheckCtx {
   bool use_s;   // sig contributes (not infinity)
 };
 
-// Writes the team's G2 register file: point R = (Q, 1, 1), Q, -Qy, Qy^2, the
+// Writes the team's G2 register file: point R = Q (projective, see below), Q, -Qy, Qy^2, the
 // Frobenius images q1 = pi(Q), -q2 = (Qx gamma2[2], Qy) (optate.go miller),
 // the G1 points and constants.
 HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
@@ -121,8 +121,13 @@ HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
     st_fp(F + R_PY * 10, C.hy);
     st_fp(F + R_SX * 10, C.sx);
     st_fp(F + R_NSY * 10, nsy);
-    put2(R_X_x, C.qx);
-    put2(R_Y_x, C.qy);
+    // R = (xi Qx : xi Qy : xi) in the projective programs' coordinates, whose
+    // Z register holds W = Z / xi = 1 (gen_g2_schedule.py prog_double_proj)
+    Fp2 xqx, xqy;
+    f2_mul_xi(xqx, C.qx);
+    f2_mul_xi(xqy, C.qy);
+    put2(R_X_x, xqx);
+    put2(R_Y_x, xqy);
     put2(R_Z_x, one2);
     put2(R_T_x, one2);
     put2(R_QX_x, C.qx);
@@ -188,29 +193,29 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   for (int i = kNafLen - 1; i > 0; i--) {
     load_fixed_line(T, F, tab, s++);
     DIAG_ADD(0);
-    x_g2<XP_DBL>(T, S, i != kNafLen - 1 ? xh<ISqr12<S_F, S_F>>() : kLinePk);
+    x_g2<XP_PDBL>(T, S, i != kNafLen - 1 ? xh<ISqr12<S_F, S_F>>() : kLinePk);
     DIAG_ADD(1);
     if (i != kNafLen - 1) x_sqr12<S_F, S_F>(T, S, kLinePk);
     DIAG_ADD(2);
     const int d = naf[i - 1];
-    const XHint step = i > 1 ? xh<IG2<XP_DBL>>() : xh<IG2<XP_ADD_F1>>();  // after this digit
-    apply_lines(T, F, C, has_fixed, S, d > 0 ? xh<IG2<XP_ADD_POS>>() : d < 0 ? xh<IG2<XP_ADD_NEG>>() : step);
+    const XHint step = i > 1 ? xh<IG2<XP_PDBL>>() : xh<IG2<XP_PADD_F1>>();  // after this digit
+    apply_lines(T, F, C, has_fixed, S, d > 0 ? xh<IG2<XP_PADD_POS>>() : d < 0 ? xh<IG2<XP_PADD_NEG>>() : step);
     DIAG_ADD(3);
     if (d != 0) {
       load_fixed_line(T, F, tab, s++);
       DIAG_ADD(0);
-      if (d > 0) x_g2<XP_ADD_POS>(T, S, kLinePk);
-      else x_g2<XP_ADD_NEG>(T, S, kLinePk);
+      if (d > 0) x_g2<XP_PADD_POS>(T, S, kLinePk);
+      else x_g2<XP_PADD_NEG>(T, S, kLinePk);
       DIAG_ADD(4);
       apply_lines(T, F, C, has_fixed, S, step);
       DIAG_ADD(3);
     }
   }
   load_fixed_line(T, F, tab, s++);
-  x_g2<XP_ADD_F1>(T, S, kLinePk);
-  apply_lines(T, F, C, has_fixed, S, xh<IG2<XP_ADD_F2>>());
+  x_g2<XP_PADD_F1>(T, S, kLinePk);
+  apply_lines(T, F, C, has_fixed, S, xh<IG2<XP_PADD_F2>>());
   load_fixed_line(T, F, tab, s++);
-  x_g2<XP_ADD_F2>(T, S, kLinePk);
+  x_g2<XP_PADD_F2>(T, S, kLinePk);
   apply_lines(T, F, C, has_fixed, S, after);
 }
 

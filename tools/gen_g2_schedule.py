@@ -211,6 +211,92 @@ def prog_add(px, py, pr2):
     return [a1, a2, a3, a4, a5]
 
 
+# ---- homogeneous projective G2 steps (the Miller loop's point R lives in X, Y, Z
+# with the Z register holding W = Z/xi, so that b' Z^2 = (3/xi) xi^2 W^2 = 3 xi W^2
+# needs no multiplication by the constant b'). Textbook formulas: Costello, Lange,
+# Naehrig (PKC 2010) doubling / add-1998-cmo-2 mixed addition, with the lines of
+# Aranha et al. (Eurocrypt 2011) for the D-type twist; each output is a lazy sum of
+# products of the previous round's values, so a doubling takes 2 rounds and an
+# addition 3 (x/crypto's Jacobian lineFunctionDouble/Add take 3 and 5). The lines
+# differ from x/crypto's by Fp2 factors and the points are the same points in other
+# coordinates; the final exponentiation removes Fp2 factors, so the pairing (and
+# every verdict) is unchanged for points of the prime-order group.
+PD = {"XY": "A", "B": "B", "U": "S", "YW": "C", "X2": "G"}            # doubling temporaries
+PA = {"TH": "AB", "LAM": "S1", "D": "D", "C": "I", "K": "S2", "N": "H", "J": "J", "V": "AV", "YL": "L1"}
+
+
+def _xi_lc(name):
+    """component lincombs of xi * name: ((3x + y), (3y - x))."""
+    x, y = comp(name, "x"), comp(name, "y")
+    return [(x, 3), (y, 1)], [(y, 3), (x, -1)]
+
+
+def prog_double_proj():
+    """T = (X : Y : xi W) -> 2T (scaled by 4) and the tangent line at (PX, PY):
+       XY, B = Y^2, U = 9 xi W^2 (= 3 b' Z^2), YW, X2 = X^2
+       X' = 2 XY (B - 3U), Y' = (B + 3U)^2 - 12 U^2, W' = 8 B YW
+       line c + b w + a w^3: c = -2 xi YW PY, b = 3 X2 PX, a = U - B"""
+    wx, wy = comp("Z", "x"), comp("Z", "y")
+    u = [Lane(comp(PD["U"], "x"), [([(wx, 6)], [(wy, 9)]), ([(wy, 9), (wx, 9)], [(wy, 1), (wx, -1)])]),
+         Lane(comp(PD["U"], "y"), [([(wy, 9), (wx, 9)], [(wy, 3), (wx, -3)]), ([(wx, -18)], [(wy, 1)])])]
+    r1 = (mul(PD["XY"], [("X", 1)], [("Y", 1)]) + sq(PD["B"], [("Y", 1)]) + u
+          + mul(PD["YW"], [("Y", 1)], [("Z", 1)]) + sq(PD["X2"], [("X", 1)]) + fixed_line_eval())
+    b, uu = PD["B"], PD["U"]
+    y3 = [Lane(comp("Y", c), sq_terms([(b, 1), (uu, 3)], c) + sq_terms([(uu, 1)], c, k=-12)) for c in "xy"]
+    cx, cy = _xi_lc(PD["YW"])
+    lc = [Lane(comp("LC", "x"), [(scale(cx, -2), scal("PY"))]), Lane(comp("LC", "y"), [(scale(cy, -2), scal("PY"))])]
+    r2 = (mul("X", [(PD["XY"], 2)], [(b, 1), (uu, -3)]) + y3 + mul("Z", [(b, 8)], [(PD["YW"], 1)])
+          + lc + smul("LB", [(PD["X2"], 3)], "PX") + lin("LA", [(uu, 1), (b, -1)]))
+    return [r1, r2]
+
+
+def prog_add_proj(px, py):
+    """T = (X : Y : xi W) -> T + (px, py) and the line through them at (PX, PY):
+       TH = Y - py xi W, LAM = X - px xi W
+       D = LAM^2, C = TH^2, K = W LAM, N = X LAM, J = TH LAM, V = W TH, YL = Y LAM
+       X' = D D + xi K C - 2 N D, Y' = J (3N - D) - xi V C - YL D, W' = K D
+       line: c = LAM PY, b = -TH PX, a = TH px - LAM py"""
+    wxi = _xi_lc("Z")
+
+    def diff(dst, base, pt):
+        # dst = base - pt * xi W
+        out = []
+        ptx, pty = comp(pt, "x"), comp(pt, "y")
+        for c in "xy":
+            if c == "x":   # (pt xi W).x = pt.x (xi W).y + pt.y (xi W).x
+                slots = [([(ptx, -1)], wxi[1]), ([(pty, -1)], wxi[0])]
+            else:          # (pt xi W).y = pt.y (xi W).y - pt.x (xi W).x
+                slots = [([(pty, -1)], wxi[1]), ([(ptx, 1)], wxi[0])]
+            out.append(Lane(comp(dst, c), slots + [([(comp(base, c), 1)], one())]))
+        return out
+
+    th, lam = PA["TH"], PA["LAM"]
+    r1 = diff(th, "Y", py) + diff(lam, "X", px) + fixed_line_eval()
+    r2 = (sq(PA["D"], [(lam, 1)]) + sq(PA["C"], [(th, 1)]) + mul(PA["K"], [("Z", 1)], [(lam, 1)])
+          + mul(PA["N"], [("X", 1)], [(lam, 1)]) + mul(PA["J"], [(th, 1)], [(lam, 1)])
+          + mul(PA["V"], [("Z", 1)], [(th, 1)]) + mul(PA["YL"], [("Y", 1)], [(lam, 1)]))
+    d, cc, k, n, j, v, yl = (PA[x] for x in ("D", "C", "K", "N", "J", "V", "YL"))
+    kx, ky = _xi_lc(k)
+    vx, vy = _xi_lc(v)
+    ccx, ccy = [(comp(cc, "x"), 1)], [(comp(cc, "y"), 1)]
+
+    def xi_times_c(ax, ay, c, sign=1):
+        # component c of sign * (ax i + ay) * C
+        if c == "x":
+            return [(scale(ax, sign), ccy), (scale(ay, sign), ccx)]
+        return [(scale(ay, sign), ccy), (scale(neg(ax), sign), ccx)]
+
+    x3 = [Lane(comp("X", c), sq_terms([(d, 1)], c) + xi_times_c(kx, ky, c) + prod_terms([(n, -2)], [(d, 1)], c))
+          for c in "xy"]
+    y3 = [Lane(comp("Y", c), prod_terms([(j, 1)], [(n, 3), (d, -1)], c) + xi_times_c(vx, vy, c, -1)
+               + prod_terms([(yl, -1)], [(d, 1)], c)) for c in "xy"]
+    la = [Lane(comp("LA", c), prod_terms([(th, 1)], [(px, 1)], c) + prod_terms([(lam, -1)], [(py, 1)], c))
+          for c in "xy"]
+    r3 = (x3 + y3 + mul("Z", [(k, 1)], [(d, 1)]) + smul("LC", [(lam, 1)], "PY") + smul("LB", [(th, -1)], "PX")
+          + la)
+    return [r1, r2, r3]
+
+
 def prog_cyc_sqr():
     """Granger-Scott squaring of f = (c0 + c3 s) + (c1 + c4 s) w + (c2 + c5 s) w^2
     (s = w^3, s^2 = xi) in the cyclotomic subgroup:
@@ -377,6 +463,11 @@ PROGRAMS = {
     "LINE_PK": prog_line("LA", "LB", "LC"),
     "LINE_FIX": prog_line("FA", "FB", "FC"),
     "CYC_SQR_X": prog_cyc_sqr_x(),
+    "PDBL": prog_double_proj(),
+    "PADD_POS": prog_add_proj("QX", "QY"),
+    "PADD_NEG": prog_add_proj("QX", "NQY"),
+    "PADD_F1": prog_add_proj("P1X", "P1Y"),
+    "PADD_F2": prog_add_proj("P2X", "QY"),
 }
 # programs also emitted in the single-phase table format (bn256_g2sched.h)
 LEGACY = ("DBL", "ADD_POS", "ADD_NEG", "ADD_F1", "ADD_F2", "CYC_SQR", "SQR12")
@@ -672,7 +763,7 @@ def run_xround(xr, F, A, B):
 X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
 SCRATCH_CAP = {"FE": 96, "ML": 48}
 X_PROGRAMS = {  # name -> (program, scratch context)
-    "DBL": "ML", "ADD_POS": "ML", "ADD_NEG": "ML", "ADD_F1": "ML", "ADD_F2": "ML",
+    "PDBL": "ML", "PADD_POS": "ML", "PADD_NEG": "ML", "PADD_F1": "ML", "PADD_F2": "ML",
     "SQR12": "ML", "LINE_PK": "ML", "LINE_FIX": "ML", "CYC_SQR": "FE", "MUL12": "FE", "CYC_SQR_X": "FE",
 }
 
@@ -726,17 +817,38 @@ def validate_x(seed=2):
         put(F, "QY", Q[1])
         put(F, "NQY", O.f2_neg(Q[1]))
         put(F, "R2", O.f2_sqr(Q[1]))
+        # projective steps: R as (x Z : y Z : Z) with Z = xi W for a random W
+        xi = (1, 3)
+        aff = lambda j: (O.f2_mul(j[0], O.f2_inv(O.f2_sqr(j[2]))),  # noqa: E731
+                         O.f2_mul(j[1], O.f2_inv(O.f2_mul(O.f2_sqr(j[2]), j[2]))))
+        rx, ry = aff(Rj)
+        Wr = (rng.randrange(1, P), rng.randrange(P))
+        Zr = O.f2_mul(xi, Wr)
+        put(F, "X", O.f2_mul(rx, Zr))
+        put(F, "Y", O.f2_mul(ry, Zr))
+        put(F, "Z", Wr)
+        put(F, "P1X", O.f2_mul(Q[0], (rng.randrange(P), rng.randrange(P))))  # any affine point works
+        put(F, "P1Y", (rng.randrange(P), rng.randrange(P)))
+
+        def check_proj(G, want_r, want_line, name):
+            zi = O.f2_inv(O.f2_mul(xi, getf(G, "Z")))
+            got = (O.f2_mul(getf(G, "X"), zi), O.f2_mul(getf(G, "Y"), zi))
+            assert got == aff(want_r), name + " point"
+            la, lb, lc = (getf(G, n) for n in ("LA", "LB", "LC"))
+            a, b, c = want_line
+            mu = O.f2_mul(la, O.f2_inv(a))   # the lines agree up to an Fp2 factor
+            assert mu != (0, 0) and (la, lb, lc) == tuple(O.f2_mul(mu, v) for v in (a, b, c)), name + " line"
+
         a, b, c, r_new = O._line_double(r, *Hp)
         G = dict(F)
-        run_xprogram(X["DBL"], G)
-        assert [getf(G, n) for n in ("X", "Y", "Z", "T")] == list(r_new), "xDBL point"
-        assert [getf(G, n) for n in ("LA", "LB", "LC")] == [a, b, c], "xDBL line"
-        for prog, pq in (("ADD_POS", (Q[0], Q[1])), ("ADD_NEG", (Q[0], O.f2_neg(Q[1])))):
+        run_xprogram(X["PDBL"], G)
+        check_proj(G, r_new, (a, b, c), "xPDBL")
+        for prog, pq in (("PADD_POS", (Q[0], Q[1])), ("PADD_NEG", (Q[0], O.f2_neg(Q[1]))),
+                         ("PADD_F1", (getf(F, "P1X"), getf(F, "P1Y")))):
             a, b, c, r_new = O._line_add(r, pq, *Hp, O.f2_sqr(pq[1]))
             G = dict(F)
             run_xprogram(X[prog], G)
-            assert [getf(G, n) for n in ("X", "Y", "Z", "T")] == list(r_new), "x" + prog
-            assert [getf(G, n) for n in ("LA", "LB", "LC")] == [a, b, c], "x" + prog + " line"
+            check_proj(G, r_new, (a, b, c), "x" + prog)
         f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
         g = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
         flat = lambda v: [z for pair in v for z in pair]  # noqa: E731
@@ -783,7 +895,7 @@ INSTANCES = sorted(set(
     + [("SQR12", ("F", "F")), ("SQR12", ("F", "A")), ("LINE_PK", ("F", "F")), ("LINE_FIX", ("F", "F"))]
     # tools/opcycles.hip
     + [("CYC_SQR_X", ("A", "A")), ("SQR12", ("A", "A")), ("LINE_PK", ("A", "A"))]
-    + [(g, ()) for g in ("DBL", "ADD_POS", "ADD_NEG", "ADD_F1", "ADD_F2")]))
+    + [(g, ()) for g in ("PDBL", "PADD_POS", "PADD_NEG", "PADD_F1", "PADD_F2")]))
 
 
 def bind(xr, binding, ctx):

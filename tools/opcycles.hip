@@ -60,8 +60,8 @@ __global__ __launch_bounds__(64) void k_op(uint32_t seed, uint32_t* sink) {
     if constexpr (OP == 11) x_mul12<S_A, S_A, S_B>(T, S, xh<IMul12<S_A, S_A, S_B>>());
     if constexpr (OP == 12) x_sqr12<S_A, S_A>(T, S, xh<ISqr12<S_A, S_A>>());
     if constexpr (OP == 13) x_line_pk<S_A, S_A>(T, S, xh<ILinePk<S_A, S_A>>());
-    if constexpr (OP == 14) x_g2<XP_DBL>(T, S, xh<IG2<XP_DBL>>());
-    if constexpr (OP == 15) x_g2<XP_ADD_POS>(T, S, xh<IG2<XP_ADD_POS>>());
+    if constexpr (OP == 14) x_g2<XP_PDBL>(T, S, xh<IG2<XP_PDBL>>());
+    if constexpr (OP == 15) x_g2<XP_PADD_POS>(T, S, xh<IG2<XP_PADD_POS>>());
     if constexpr (OP == 9) {
       Fp v;
       ld_fp(v, slot(T, S_A) + T.e * 10);
