@@ -79,6 +79,47 @@ def make_batch(eng: Engine, n: int, seed: int):
     return pks, bytes(sigs), expect
 
 
+def make_aggregate_batch(eng: Engine, n_reg: int, n: int, seed: int):
+    """a registry of n_reg keys and n incoming
+    multisignatures as Handel's evaluator receives them: for each, a random
+    node's random non-empty level (partitioner rangeLevel, partitioner.go:133-178),
+    a bitset of density U[0.5, 1.0] over the level's registry range, and the
+    aggregate signature of the set bits (sum of the secret keys times H(msg));
+    1/8 of the aggregates tampered (+ G1)."""
+    from handel_amd.partitioner import bits_to_words, level_sizes
+
+    rng = np.random.default_rng(seed)
+    kb = seeded_scalars(n_reg, seed)
+    reg = eng.keygen(kb)
+    assert not eng.registry_load(reg).any()
+    limbs = np.frombuffer(kb, dtype=">u4").reshape(n_reg, 8)[:, ::-1].astype(np.int64)  # LE 32-bit limbs
+    reqs, words, scalars, signers = [], [], bytearray(), []
+    nodes = rng.integers(0, n_reg, size=n)
+    for i in range(n):
+        levels = level_sizes(int(nodes[i]), n_reg)
+        _, lo, hi = levels[rng.integers(len(levels))]
+        bits = rng.random(hi - lo) < rng.uniform(0.5, 1.0)
+        bits[rng.integers(hi - lo)] = True
+        signers.append(int(bits.sum()))
+        col = limbs[lo:hi][bits].sum(axis=0)
+        k = sum(int(v) << (32 * j) for j, v in enumerate(col)) % ORDER
+        w = bits_to_words(bits)
+        reqs.append((lo, hi - lo, hi - lo, len(words)))
+        words.extend(int(x) for x in w)
+        scalars += k.to_bytes(32, "big")
+    sigs = bytearray(eng.sign(bytes(scalars)))
+    idx = list(range(0, n, 8))
+    bad, codes = eng.combine_g1(b"".join(bytes(sigs[64 * i:64 * i + 64]) for i in idx), G1_GEN_BYTES * len(idx))
+    assert not codes.any()
+    for j, i in enumerate(idx):
+        sigs[64 * i:64 * i + 64] = bad[64 * j:64 * j + 64]
+    expect = np.zeros(n, dtype=np.int32)
+    expect[idx] = 1
+    from handel_amd.engine import REQ_DTYPE
+
+    return np.array(reqs, dtype=REQ_DTYPE), np.array(words, dtype=np.uint64), bytes(sigs), expect, np.array(signers)
+
+
 def pmc_traffic():
     """HBM bytes per k_verify launch from the newest committed PMC summary
     (profiles/*_pmc.csv, written by tools/profile_round.sh +
@@ -120,6 +161,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-aggregate", action="store_true", help="skip the config-3 aggregate-verify line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,6 +229,47 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": "k_verify", "kernel_ms": round(avg_kernel_ms, 4),
                 "work_per_check": f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads"}
+    # config 3: aggregate verification of Handel multisignatures on a
+    # 4000-key registry — bitset-driven G2 Combine + pairing check, inputs resident
+    aggregate = None
+    if not args.no_aggregate:
+        reqs, words, asigs, aexpect, sizes = make_aggregate_batch(eng, 4000, n, seed=4321 + rank)
+        d_reqs = torch.frombuffer(bytearray(reqs.tobytes()), dtype=torch.uint8).to(dev)
+        d_words = torch.frombuffer(bytearray(words.tobytes()), dtype=torch.uint8).to(dev)
+        d_asigs = torch.frombuffer(bytearray(asigs), dtype=torch.uint8).to(dev)
+        d_acodes = torch.zeros(n, dtype=torch.int32, device=dev)
+
+        def astep():
+            eng.verify_aggregate_device(d_reqs.data_ptr(), n, d_words.data_ptr(), d_asigs.data_ptr(),
+                                        d_acodes.data_ptr(), 0, stream.cuda_stream)
+
+        for _ in range(args.warmup):
+            astep()
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(d_acodes.cpu().numpy(), aexpect), "aggregate verdicts differ from the expected pattern"
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            astep()
+        torch.cuda.synchronize(dev)
+        if dist:
+            tdist.barrier()
+        adt = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([adt], dtype=torch.float64, device=dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            adt = float(t.item())
+        assert np.array_equal(d_acodes.cpu().numpy(), aexpect)
+        aggregate = {"metric": "BN254 aggregate-sig verifications/sec (Handel multisigs, 4000-key registry)",
+                     "value": round(n * args.steps * world / adt, 1), "unit": "verifications/s",
+                     "ms_per_step": round(adt / args.steps * 1e3, 4),
+                     "workload": f"config 3: {n} multisigs per GPU, random node/level of a 4000-node Handel "
+                                 f"registry, bitset density U[0.5,1], 1/8 tampered",
+                     "signers_per_check_mean": round(float(sizes.mean()), 1),
+                     "signers_per_check_max": int(sizes.max())}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
@@ -211,6 +294,7 @@ def main():
                        "batch_per_gpu": n, "message": "lib.Message (81 B)", "parallelism": f"dp{world} (replicated registry, sharded batches)"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "aggregate": aggregate,
         }
         print(json.dumps(line))
     eng.close()

@@ -221,68 +221,240 @@ __global__ void k_g2_lines(LineCoef* tab) {
 }
 
 // ------------------------------------------------------------------ aggregation
-// One 64-lane workgroup per request: lane l folds the registry points whose
-// bit i has i % 64 == l with mixed additions, then an LDS tree reduction
-// combines the 64 partial sums. The result is converted to affine by lane 0.
-// Complement trick: when more than half the bits are set and a precomputed
-// aligned block sum covers the request's range, sum = block - sum(unset).
-__global__ __launch_bounds__(64) void k_aggregate(const PointG2* reg, int nreg, const AggRequest* reqs, int n,
-                                                  const uint64_t* words, CheckIn* out, int32_t* codes) {
-  __shared__ G2J part[64];
-  int r = blockIdx.x;
-  if (r >= n) return;
-  AggRequest q = reqs[r];
-  int lane = threadIdx.x;
-  bool bad = (codes[r] != HG_OK);
-  G2J acc;
-  g2_set_inf(acc);
-  uint32_t any = 0;
-  if (!bad) {
-    for (uint32_t i = lane; i < q.bitlen; i += 64) {
-      uint64_t w = words[q.word_offset + (i >> 6)];
-      if ((w >> (i & 63)) & 1) {
-        any = 1;
-        const PointG2& P = reg[q.offset + i];
-        if (P.inf) continue;
-        if (g2_is_inf(acc)) {
-          acc.x = P.x;
-          acc.y = P.y;
-          f2_one(acc.z);
-        } else {
-          g2_add_affine(acc, acc, P.x, P.y);
-        }
-      }
+// The aggregate key of a request is the group sum of the registry keys whose
+// bit is set (processing.go:355-363 folds PublicKey.Combine over them; the
+// affine result is the same for any summation order).
+//
+// Block sums: Handel's level ranges are aligned power-of-two registry blocks
+// clipped at N (partitioner.go:133-178), so hg_registry_load precomputes the
+// sum of every aligned block [j 2^k, min((j+1) 2^k, N)) (k_block_sums, one
+// level per launch). When more than half of a block-aligned request's bits are
+// set, the kernel folds the UNSET keys and returns block - fold.
+//
+// k_aggregate, one 64-lane workgroup per request:
+//   1. popcount of the bitset (lane-strided words, LDS reduction) -> set count,
+//      complement decision, m = number of keys to fold;
+//   2. compaction of the folded positions into LDS (per-word prefix offsets), so
+//      lanes fold consecutive entries with no divergence on unset bits;
+//   3. L = pow2 ~ m/2 lanes fold ceil(m/L) keys each with mixed additions, then a
+//      log2(L)-level LDS tree of full additions (few levels for small requests);
+//   4. lane 0 applies the block complement and converts to affine.
+struct AggPartial {
+  G2J s;          // fold of the set (or, complemented, the unset) keys
+  uint32_t cnt;   // set bits
+  int comp, k;    // complement at block level k
+};
+struct BlockIndex {
+  int base[24];  // level k block j at blocks[base[k] + j]; level 0 is the registry
+  int levels;    // highest level with a table
+};
+
+__global__ void k_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ndst) return;
+  const PointG2& a = src[2 * j];
+  G2J s;
+  if (a.inf) g2_set_inf(s);
+  else { s.x = a.x; s.y = a.y; f2_one(s.z); }
+  if (2 * j + 1 < nsrc && !src[2 * j + 1].inf) g2_add_affine(s, s, src[2 * j + 1].x, src[2 * j + 1].y);
+  PointG2 o;
+  o.pad[0] = o.pad[1] = o.pad[2] = 0;
+  if (g2_is_inf(s)) {
+    f2_zero(o.x);
+    f2_zero(o.y);
+    o.inf = 1;
+  } else {
+    g2_affine(o.x, o.y, s);
+    o.inf = 0;
+  }
+  dst[j] = o;
+}
+
+static constexpr int kAggPosCap = 4096;  // folded positions staged per pass (64 words)
+
+// The per-request plan shared by the ordering and the fold kernels: set count,
+// whether the block complement applies (and at which level), keys to fold m,
+// and the lanes L that fold them.
+struct AggPlan {
+  uint32_t cnt, m;
+  int k, lanes;
+  bool comp;
+};
+HG_DEV uint64_t agg_word(const AggRequest& q, const uint64_t* words, uint32_t wi) {
+  uint64_t w = words[q.word_offset + wi];
+  const uint32_t lo = wi * 64;
+  if (lo + 64 > q.bitlen) w &= (1ull << (q.bitlen - lo)) - 1;
+  return w;
+}
+HG_DEV AggPlan agg_plan(const AggRequest& q, uint32_t cnt, int nreg, int levels) {
+  AggPlan p;
+  p.cnt = cnt;
+  const uint32_t bitlen = q.bitlen;
+  int k = 0;
+  while (k < 31 && (1u << k) < bitlen) k++;
+  const bool aligned = bitlen > 0 && k <= levels && (q.offset & ((1u << k) - 1)) == 0 &&
+                       (bitlen == (1u << k) || q.offset + bitlen == (uint32_t)nreg);
+  p.k = k;
+  p.comp = aligned && k > 0 && 2 * cnt > bitlen;
+  p.m = p.comp ? bitlen - cnt : cnt;
+  int L = 1;
+  while (L < 64 && 2u * (uint32_t)(2 * L) <= p.m + 1) L *= 2;  // L ~ m / 2, power of two
+  p.lanes = L;
+  return p;
+}
+
+// Longest-processing-time-first order of the requests (one 1024-thread block):
+// a counting sort on the estimated fold cost, so the heaviest requests start
+// first and the light ones fill in behind them.
+__global__ __launch_bounds__(1024) void k_agg_order(const AggRequest* reqs, int n, const uint64_t* words,
+                                                    const int32_t* codes, int nreg, int levels, int* order) {
+  __shared__ int hist[64];
+  __shared__ int start[64];
+  const int tid = threadIdx.x;
+  if (tid < 64) hist[tid] = 0;
+  __syncthreads();
+  auto bucket = [&](int r) -> int {
+    if (codes[r] != HG_OK) return 63;
+    const AggRequest q = reqs[r];
+    uint32_t cnt = 0;
+    for (uint32_t wi = 0; wi < (q.bitlen + 63) / 64; wi++) cnt += __popcll(agg_word(q, words, wi));
+    AggPlan p = agg_plan(q, cnt, nreg, levels);
+    int lg = 0;
+    while ((1 << lg) < p.lanes) lg++;
+    // fold cost in tenths of a full addition: ceil(m / L) mixed (~0.65) + log2(L) full
+    const int cost = ((int)((p.m + p.lanes - 1) / p.lanes) * 13 + lg * 20) / 4;
+    return 63 - (cost < 63 ? cost : 63);
+  };
+  for (int r = tid; r < n; r += blockDim.x) atomicAdd(&hist[bucket(r)], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < 64; b++) {
+      start[b] = acc;
+      acc += hist[b];
     }
   }
-  part[lane] = acc;
-  uint64_t anyb = __ballot(any != 0);
   __syncthreads();
-  for (int s = 32; s > 0; s >>= 1) {
-    if (lane < s) {
-      G2J o = part[lane + s];
-      G2J m = part[lane];
-      g2_add(m, m, o);
-      part[lane] = m;
+  for (int r = tid; r < n; r += blockDim.x) order[atomicAdd(&start[bucket(r)], 1)] = r;
+}
+
+__global__ __launch_bounds__(64) void k_aggregate(const PointG2* reg, int nreg, BlockIndex bi,
+                                                  const AggRequest* reqs, int n, const uint64_t* words,
+                                                  const int* order, AggPartial* partial, const int32_t* codes) {
+  __shared__ G2J part[64];
+  __shared__ uint16_t pos[kAggPosCap];
+  __shared__ uint32_t cnt_lds[64];
+  if ((int)blockIdx.x >= n) return;
+  const int r = order[blockIdx.x];
+  const AggRequest q = reqs[r];
+  const int lane = threadIdx.x;
+  if (codes[r] != HG_OK) return;  // level error: no aggregate (uniform exit)
+  const uint32_t bitlen = q.bitlen;
+  const uint32_t nwords = (bitlen + 63) / 64;
+  auto word_at = [&](uint32_t wi) -> uint64_t { return agg_word(q, words, wi); };
+  // 1. set count
+  uint32_t c = 0;
+  for (uint32_t wi = lane; wi < nwords; wi += 64) c += __popcll(word_at(wi));
+  cnt_lds[lane] = c;
+  __syncthreads();
+  for (int s2 = 32; s2 > 0; s2 >>= 1) {
+    if (lane < s2) cnt_lds[lane] += cnt_lds[lane + s2];
+    __syncthreads();
+  }
+  const uint32_t cnt = cnt_lds[0];
+  __syncthreads();
+  const AggPlan plan = agg_plan(q, cnt, nreg, bi.levels);
+  const bool comp = plan.comp;
+  const int k = plan.k, L = plan.lanes;
+  // 2.-3. fold the complement / set keys, 64 words (4096 positions) per pass
+  G2J acc;
+  g2_set_inf(acc);
+  for (uint32_t w0 = 0; w0 < nwords; w0 += 64) {
+    const uint32_t wi = w0 + lane;
+    uint64_t mb = 0;
+    if (wi < nwords) {
+      mb = word_at(wi);
+      if (comp) {
+        mb = ~mb;
+        const uint32_t lo = wi * 64;
+        if (lo + 64 > bitlen) mb &= (1ull << (bitlen - lo)) - 1;
+      }
+    }
+    // exclusive prefix of per-word counts (Hillis-Steele in LDS)
+    uint32_t pc = __popcll(mb);
+    cnt_lds[lane] = pc;
+    __syncthreads();
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t v = lane >= d ? cnt_lds[lane - d] : 0;
+      __syncthreads();
+      cnt_lds[lane] += v;
+      __syncthreads();
+    }
+    const uint32_t total = cnt_lds[63];
+    uint32_t at = cnt_lds[lane] - pc;
+    while (mb) {
+      const int b = __builtin_ctzll(mb);
+      pos[at++] = (uint16_t)(lane * 64 + b);
+      mb &= mb - 1;
+    }
+    __syncthreads();
+    if (lane < L) {
+      for (uint32_t t = lane; t < total; t += L) {
+        const PointG2& P = reg[q.offset + w0 * 64 + pos[t]];
+        if (!P.inf) g2_madd(acc, acc, P.x, P.y);
+      }
     }
     __syncthreads();
   }
+  part[lane] = acc;
+  __syncthreads();
+  for (int s2 = L / 2; s2 > 0; s2 >>= 1) {
+    if (lane < s2) {
+      G2J o = part[lane + s2];
+      G2J mm = part[lane];
+      g2_add(mm, mm, o);
+      part[lane] = mm;
+    }
+    __syncthreads();
+  }
+  // 4. the root partial; k_agg_finish applies the complement and converts to affine
   if (lane == 0) {
-    CheckIn& C = out[r];
-    if (bad) return;
-    if (anyb == 0) {
-      codes[r] = HG_ERR_EMPTY_AGG;
-      C.pk.inf = 1;
-      return;
-    }
-    G2J s = part[0];
-    if (g2_is_inf(s)) {
-      C.pk.inf = 1;
-      f2_zero(C.pk.x);
-      f2_zero(C.pk.y);
-    } else {
-      g2_affine(C.pk.x, C.pk.y, s);
-      C.pk.inf = 0;
-    }
+    AggPartial& o = partial[r];
+    o.s = part[0];
+    o.cnt = cnt;
+    o.comp = comp ? 1 : 0;
+    o.k = k;
+  }
+}
+
+// One thread per request: block - fold for complemented requests, affine
+// conversion (Bernstein-Yang inversion), empty-aggregate code.
+__global__ void k_agg_finish(const PointG2* blocks, BlockIndex bi, const AggRequest* reqs, int n,
+                             const AggPartial* partial, CheckIn* out, int32_t* codes) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n || codes[r] != HG_OK) return;
+  const AggPartial& pa = partial[r];
+  CheckIn& C = out[r];
+  if (pa.cnt == 0) {
+    codes[r] = HG_ERR_EMPTY_AGG;
+    C.pk.inf = 1;
+    return;
+  }
+  G2J S = pa.s;
+  if (pa.comp) {
+    const PointG2& B = blocks[bi.base[pa.k] + (reqs[r].offset >> pa.k)];
+    G2J nf = S;
+    f2_neg(nf.y, S.y);
+    if (B.inf) S = nf;
+    else g2_madd(S, nf, B.x, B.y);
+  }
+  if (g2_is_inf(S)) {
+    C.pk.inf = 1;
+    f2_zero(C.pk.x);
+    f2_zero(C.pk.y);
+  } else {
+    g2_affine(C.pk.x, C.pk.y, S);
+    C.pk.inf = 0;
   }
 }
 
@@ -390,9 +562,21 @@ void launch_g1_mul(const PointG1* base, const uint8_t* scalars, int n, PointG1* 
 }
 void launch_hash_point(const uint32_t* k, PointG1* out, hipStream_t s) { k_hash_point<<<1, 64, 0, s>>>(k, out); }
 void launch_g2_lines(LineCoef* tab, hipStream_t s) { k_g2_lines<<<1, 64, 0, s>>>(tab); }
-void launch_aggregate(const PointG2* reg, int nreg, const AggRequest* reqs, int n, const uint64_t* words,
+void launch_aggregate(const PointG2* reg, int nreg, const PointG2* blocks, const int* block_base, int levels,
+                      const AggRequest* reqs, int n, const uint64_t* words, int* order, void* partial_ws,
                       CheckIn* out, int32_t* codes, hipStream_t s) {
-  if (n > 0) k_aggregate<<<n, 64, 0, s>>>(reg, nreg, reqs, n, words, out, codes);
+  AggPartial* partial = (AggPartial*)partial_ws;
+  BlockIndex bi;
+  bi.levels = levels < 23 ? levels : 23;
+  for (int k = 0; k < 24; k++) bi.base[k] = k <= bi.levels ? block_base[k] : 0;
+  if (n <= 0) return;
+  k_agg_order<<<1, 1024, 0, s>>>(reqs, n, words, codes, nreg, bi.levels, order);
+  k_aggregate<<<n, 64, 0, s>>>(reg, nreg, bi, reqs, n, words, order, partial, codes);
+  k_agg_finish<<<nblk(n, 64), 64, 0, s>>>(blocks, bi, reqs, n, partial, out, codes);
+}
+size_t agg_partial_bytes() { return sizeof(AggPartial); }
+void launch_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst, hipStream_t s) {
+  if (ndst > 0) k_block_sums<<<nblk(ndst, 64), 64, 0, s>>>(src, nsrc, dst, ndst);
 }
 void launch_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t* out, hipStream_t s) {
   if (n > 0) k_g1_combine<<<nblk(n, 64), 64, 0, s>>>(a, b, n, out);

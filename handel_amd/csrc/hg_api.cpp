@@ -156,6 +156,10 @@ struct hg_ctx {
   // registry
   DevBuf<PointG2> reg;
   size_t nreg = 0;
+  // aligned block sums of the registry (level k block j at blocks[block_base[k] + j])
+  DevBuf<PointG2> blocks;
+  std::vector<int> block_base = std::vector<int>(24, 0);
+  int block_levels = 0;
   // workspaces
   DevBuf<uint8_t> bytes_a, bytes_b;
   DevBuf<PointG2> pts2;
@@ -163,6 +167,8 @@ struct hg_ctx {
   DevBuf<CheckIn> checks;
   DevBuf<int32_t> codes_a, codes_b, codes_c;
   DevBuf<hg_request> reqs;
+  DevBuf<int> order;  // aggregation schedule (k_agg_order)
+  DevBuf<uint8_t> agg_ws;  // per-request fold results (k_aggregate -> k_agg_finish)
   DevBuf<uint64_t> words;
   // optional per-launch timing of the pairing-check kernel (bench roofline)
   bool timing = false;
@@ -316,10 +322,33 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   for (size_t i = 0; i < n; i++) bad |= h[i] != HG_OK;
   if (codes && n) memcpy(codes, h.data(), n * 4);
   c->nreg = n;
+  c->block_levels = 0;
   if (bad) {
     c->err = "registry contains keys that fail to unmarshal";
     return HG_ERR_PK_UNMARSHAL;
   }
+  // sums of the aligned power-of-two blocks (Handel's level ranges), level by level
+  int K = 0;
+  while (K < 23 && ((size_t)1 << K) < n) K++;
+  std::vector<size_t> nb(K + 1, 0);
+  nb[0] = n;
+  size_t total = 0;
+  for (int k = 1; k <= K; k++) {
+    nb[k] = (n + ((size_t)1 << k) - 1) >> k;
+    c->block_base[k] = (int)total;
+    total += nb[k];
+  }
+  if (total) {
+    HG_CHECK(c, c->blocks.ensure(total));
+    for (int k = 1; k <= K; k++) {
+      const PointG2* src = k == 1 ? c->reg.p : c->blocks.p + c->block_base[k - 1];
+      launch_block_sums(src, (int)nb[k - 1], c->blocks.p + c->block_base[k], (int)nb[k], c->stream);
+    }
+    rc = check_launch(c);
+    if (rc) return rc;
+    HG_CHECK(c, hipStreamSynchronize(c->stream));
+  }
+  c->block_levels = K;
   return HG_OK;
 }
 
@@ -390,7 +419,10 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
                                    const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
                                    bool verify, hipStream_t s) {
   HG_CHECK(c, c->checks.ensure(n));
-  launch_aggregate(c->reg.p, (int)c->nreg, d_reqs, (int)n, d_words, c->checks.p, d_lvl, s);
+  HG_CHECK(c, c->order.ensure(n));
+  HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes()));
+  launch_aggregate(c->reg.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
+                   d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
   if (d_agg) {
     HG_CHECK(c, c->pts2.ensure(n));
     launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);

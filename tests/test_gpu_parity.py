@@ -184,3 +184,53 @@ def test_verify_aggregate_matches_oracle(engine):
 def engine_req_dtype():
     from handel_amd.engine import REQ_DTYPE
     return REQ_DTYPE
+
+
+def test_aggregate_block_complement_matches_oracle(engine):
+    """Level ranges of a 300-key registry (aligned blocks, clipped last blocks,
+    multi-word bitsets) at densities that take the block-sum complement path
+    (all set, all but one, just over half) and the direct path (half, one bit),
+    with a duplicated key (doubling inside the fold) and an infinity key."""
+    n_reg = 300
+    ks = F.scalars(n_reg, seed=b"agg-blocks")
+    ks[17] = ks[16]                        # duplicate registry key
+    reg = bytearray(R.g2_scalar_base(F.scalar_bytes(ks)))
+    reg[128 * 40:128 * 41] = bytes(128)    # infinity key (all-zero marshal)
+    reg = bytes(reg)
+    assert list(engine.registry_load(reg)) == [0] * n_reg
+    msg = F.LIB_MESSAGE
+    assert engine.set_message(msg) == 0
+    ranges = []
+    for node in (0, 5, 77, 150, 299):
+        for lvl in range(1, O.log2_ceil(n_reg) + 1):
+            rl, err = O.range_level(node, n_reg, lvl)
+            if err is None:
+                ranges.append((rl[0], rl[1] - rl[0]))
+    ranges.append((0, n_reg))
+    ranges = sorted(set(ranges))
+    rng = np.random.default_rng(11)
+    bitsets = []
+    for i, (off, size) in enumerate(ranges):
+        kind = i % 5
+        if kind == 0:
+            bits = [True] * size
+        elif kind == 1:
+            bits = [True] * size
+            bits[int(rng.integers(size))] = False
+        elif kind == 2:
+            bits = list(rng.permutation([True] * (size // 2 + 1) + [False] * (size - size // 2 - 1)))
+        elif kind == 3:
+            bits = list(rng.permutation([True] * (size // 2) + [False] * (size - size // 2)))
+        else:
+            bits = [False] * size
+            bits[int(rng.integers(size))] = True
+        bitsets.append([bool(b) for b in bits])
+    reqs, words = F.pack_requests(ranges, bitsets)
+    sigs = O.g1_marshal(O.G1_GEN) * len(reqs)
+    codes, agg = engine.verify_aggregate(np.array(reqs, dtype=engine_req_dtype()), words, sigs, want_agg=True)
+    woff = np.array([r[3] for r in reqs], dtype=np.uint64)
+    want, want_agg = R.verify_aggregate(msg, reg, [r[0] for r in reqs], [r[1] for r in reqs],
+                                        [r[2] for r in reqs], words, woff, sigs, nthreads=4, want_agg=True)
+    assert list(codes) == list(want)
+    for i in range(len(reqs)):
+        assert agg[128 * i:128 * (i + 1)] == want_agg[128 * i:128 * (i + 1)], f"agg {i} {ranges[i]}"
