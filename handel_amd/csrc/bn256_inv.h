@@ -147,6 +147,9 @@ HG_HD void update_fg_62_var(int len, S62* f, S62* g, const Mat* t) {
   cg = (__int128)q * fi + (__int128)r * gi;
   cf >>= 62;
   cg >>= 62;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
   for (int i = 1; i < len; ++i) {
     fi = f->v[i];
     gi = g->v[i];
@@ -208,37 +211,24 @@ HG_HD void normalize_62(S62* r, int64_t sign) {
   r->v[4] = r4;
 }
 
-// x <- x^-1 mod p for 0 <= x < p (0 -> 0)
+// x <- x^-1 mod p for 0 <= x < p (0 -> 0). All five limbs of f and g are
+// always updated (no length shortening): every limb index is a constant after
+// unrolling, so the device code keeps f, g, d, e in registers.
 HG_HD void modinv_var(S62* x) {
   const int64_t P[5] = {HG_P62};
   S62 d = {{0, 0, 0, 0, 0}};
   S62 e = {{1, 0, 0, 0, 0}};
   S62 f = {{P[0], P[1], P[2], P[3], P[4]}};
   S62 g = *x;
-  int len = 5;
   int64_t eta = -1;  // eta = -delta, delta = 1
   for (;;) {
     Mat t;
     eta = divsteps_62_var(eta, (uint64_t)f.v[0], (uint64_t)g.v[0], &t);
     update_de_62(&d, &e, &t);
-    update_fg_62_var(len, &f, &g, &t);
-    if (g.v[0] == 0) {
-      int64_t cond = 0;
-      for (int j = 1; j < len; ++j) cond |= g.v[j];
-      if (cond == 0) break;
-    }
-    // shorten f, g when both top limbs are sign-only
-    const int64_t fn = f.v[len - 1], gn = g.v[len - 1];
-    int64_t cond = ((int64_t)len - 2) >> 63;
-    cond |= fn ^ (fn >> 63);
-    cond |= gn ^ (gn >> 63);
-    if (cond == 0) {
-      f.v[len - 2] = (int64_t)((uint64_t)f.v[len - 2] | ((uint64_t)fn << 62));
-      g.v[len - 2] = (int64_t)((uint64_t)g.v[len - 2] | ((uint64_t)gn << 62));
-      --len;
-    }
+    update_fg_62_var(5, &f, &g, &t);
+    if ((g.v[0] | g.v[1] | g.v[2] | g.v[3] | g.v[4]) == 0) break;
   }
-  normalize_62(&d, f.v[len - 1]);
+  normalize_62(&d, f.v[4]);
   *x = d;
 }
 

@@ -4,4 +4,4 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 &&
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err &&
-bash tools/profile_round.sh r01_v4
+bash tools/profile_round.sh "${1:-r01}"
