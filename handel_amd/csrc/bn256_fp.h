@@ -7,15 +7,18 @@
 //
 // Representation (chosen for v_mad_u64_u32, which is half-rate on gfx950):
 //   * an element is 10 limbs of 26 bits (little-endian), Montgomery form with
-//     R = 2^260, fully reduced to [0, p) unless a function says otherwise;
-//   * a product is accumulated column-wise into 20 x 64-bit accumulators
+//     R = 2^286 (11 REDC digits), fully reduced to [0, p) unless a function
+//     says otherwise;
+//   * a product is accumulated column-wise into 21 x 64-bit accumulators
 //     (`Acc`). Each 26x26-bit partial product is ONE in-place
 //     v_mad_u64_u32 with no carry handling, and a column has room for 2^12
 //     partial products, so a sum of up to 16 products of reduced operands
 //     is reduced ONCE (lazy reduction) — the Fp12 coefficient sums, the Fp2
 //     schoolbook products and the squarings all use that.
-//   * Montgomery REDC of T < 16 p^2 with R = 2^260 > 16 p returns a value
-//     < 2p, and one conditional subtraction makes it canonical.
+//   * Montgomery REDC of T < p R (R = 2^286 ~ 2^30.5 p, so any lazy sum the
+//     code forms) returns a value < 2p, and one conditional subtraction makes
+//     it canonical. The 11th digit costs 10 mads and saves a quotient-estimate
+//     reduction after every lazy sum.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,7 +34,7 @@ struct Fp {
   uint32_t l[10];
 };
 struct Acc {
-  uint64_t c[20];
+  uint64_t c[21];  // product columns 0..18, REDC digits up to 19, R-shifted terms 11..20
 };
 
 static constexpr uint32_t kPLimbsC[10] = {HG_PLIMBS};
@@ -90,7 +93,7 @@ HG_DEV void fp_csub(Fp& r, const uint32_t* x) {
 // ---------------------------------------------------------------- accumulators
 HG_DEV void acc_zero(Acc& a) {
 #pragma unroll
-  for (int i = 0; i < 20; i++) a.c[i] = 0;
+  for (int i = 0; i < 21; i++) a.c[i] = 0;
 }
 // a += x * y (limbs of x, y may be up to 27 bits: sums of two reduced values)
 HG_DEV void acc_mad(Acc& a, const Fp& x, const Fp& y) {
@@ -111,10 +114,12 @@ HG_DEV void acc_sqr(Acc& a, const Fp& x) {
     for (int j = i + 1; j < 10; j++) a.c[i + j] += (uint64_t)x.l[i] * d[j];
   }
 }
-// Montgomery REDC: r = T * 2^-260 mod p, canonical. Requires T < 16 p^2.
+// Montgomery REDC: r = T * 2^-286 mod p, canonical. Requires T < p R
+// (11 digits of 26 bits; the result T / R + q p / R < 2p before the final
+// conditional subtraction).
 HG_DEV void acc_reduce(Fp& r, Acc& a) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) {
+  for (int i = 0; i < kRedcSteps; i++) {
     uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
 #pragma unroll
     for (int j = 0; j < 10; j++) a.c[i + j] += (uint64_t)q * p_limb(j);
@@ -124,7 +129,7 @@ HG_DEV void acc_reduce(Fp& r, Acc& a) {
   uint64_t carry = 0;
 #pragma unroll
   for (int j = 0; j < 10; j++) {
-    uint64_t v = a.c[10 + j] + carry;
+    uint64_t v = a.c[kRedcSteps + j] + carry;
     x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
     carry = v >> 26;
   }

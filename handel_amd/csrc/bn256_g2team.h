@@ -15,7 +15,7 @@
 
 namespace hg {
 
-// Montgomery REDC for T < ~199 p^2 (output < 8p), then full reduction.
+// Montgomery REDC of a lazy sum (T < p R), canonical result.
 HG_DEV void acc_reduce8(Fp& r, Acc& a) { acc_reduce_wide(r, a); }
 
 // sum_m c_m * F[r_m] + K p  (K = sum of the negative |c_m|): a non-negative

@@ -59,7 +59,7 @@ HG_DEV Team make_team(uint32_t* lds_base, int words_per_team) {
   return T;
 }
 
-// Reduce a normalized-limb value < 8p (limb 9 holds the top bits) to [0, p):
+// Reduce a normalized-limb value < 31p (limb 9 holds the top bits) to [0, p):
 // q = floor(top / (p9 + 1)) underestimates floor(value / p) by at most one,
 // so one conditional subtraction finishes.
 HG_DEV void fp_reduce8(Fp& r, const uint32_t* x) {
@@ -76,10 +76,13 @@ HG_DEV void fp_reduce8(Fp& r, const uint32_t* x) {
   fp_csub(r, y);
 }
 
-// Montgomery REDC for T < ~199 p^2 (output < 8p), then full reduction.
+// REDC of a lazy sum that carries R-shifted linear terms (acc_add_shifted):
+// those pass through REDC unchanged, so the result is < (products / R) +
+// (linear terms) + p, below 31p (generator-checked); a quotient estimate
+// (fp_reduce8) makes it canonical. Sums of products only use acc_reduce.
 HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) {
+  for (int i = 0; i < kRedcSteps; i++) {
     uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
 #pragma unroll
     for (int j = 0; j < 10; j++) a.c[i + j] += (uint64_t)q * p_limb(j);
@@ -89,7 +92,7 @@ HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
   uint64_t carry = 0;
 #pragma unroll
   for (int j = 0; j < 10; j++) {
-    uint64_t v = a.c[10 + j] + carry;
+    uint64_t v = a.c[kRedcSteps + j] + carry;
     x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
     carry = v >> 26;
   }
@@ -157,11 +160,11 @@ HG_DEV void t12_mul(const Team& T, int dst, int sa, int sb) {
 
 HG_DEV void t12_sqr(const Team& T, int dst, int sa) { t12_mul(T, dst, sa, sa); }
 
-// acc += v * R (R = 2^260 = 2^(26*10)): adds the Montgomery-form value v to
+// acc += v * R (R = 2^286 = 2^(26*11)): adds the Montgomery-form value v to
 // the product sum, i.e. a linear term costs 10 adds instead of a product.
 HG_DEV void acc_add_shifted(Acc& acc, const Fp& v) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) acc.c[10 + i] += v.l[i];
+  for (int i = 0; i < 10; i++) acc.c[kRedcSteps + i] += v.l[i];
 }
 
 // small constant multiple of a loose element, limb-wise (no carries)

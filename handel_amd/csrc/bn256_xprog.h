@@ -16,8 +16,8 @@
 // limb-wise without carries: (2p)'' below is 2p with limbs in [2^26, 2^27 + 2^26)
 // (top limb 2 p_9 - 1), so (2p)''_l - x_l >= 0 for every canonical x. The
 // generator bounds every limb sum below 2^32, every 64-bit column below 2^64
-// and every REDC input below 800 p^2 (acc_reduce_wide's exact range, < 31 p
-// after REDC).
+// and the REDC result: below 2p for product-only rounds (acc_reduce: one
+// conditional subtraction), below 31p with linear terms (acc_reduce_wide).
 //
 // Every table is bound to one call site: operands are absolute positions in
 // the team region (Fp12 slot s element e -> element 12 s + e, register r ->
@@ -160,11 +160,12 @@ HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
     uint32_t val[10];
     x_lincomb<W, NL>(T, w, lbase, val);
 #pragma unroll
-    for (int l = 0; l < 10; l++) acc.c[10 + l] += val[l];
+    for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] += val[l];
   }
   const uint32_t dst = x_off(w, lbase + NL);
   Fp r;
-  acc_reduce_wide(r, acc);
+  if constexpr (NL > 0) acc_reduce_wide(r, acc);  // linear terms: result < 31p
+  else acc_reduce(r, acc);                        // products only: < 2p, one subtraction
   team_sync();
   if (dst != 0xffffu) st_fp(x_at(T, dst), r);
   team_sync();

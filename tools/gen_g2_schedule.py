@@ -34,7 +34,8 @@ import random
 import sys
 
 P = 65000549695646603732796438742359905742825358107623003571877145026864184071783
-R_OVER_P = (1 << 260) / P  # REDC(T) < T/R + p
+R_BITS = 286  # Montgomery R = 2^286 (11 REDC digits, bn256_constants.h kRedcSteps)
+R_OVER_P = (1 << R_BITS) / P  # REDC(T) < T/R + p
 MAX_NSLOT = 7
 MAX_TERMS = 6
 SLOT_A = 128
@@ -494,8 +495,8 @@ def check_round(lanes, name):
                 negs = sum(-k for _, k in terms if k < 0)
                 assert pos + negs <= 30, f"{name}: coefficient range {terms}"
             t += bound(a) * bound(b)
-        # REDC output < (t / R_OVER_P + 1) p must stay below 8p (fp_reduce8)
-        assert t / R_OVER_P + 1 < 8, f"{name}: product bound {t}"
+        # REDC output < (t / R_OVER_P + 1) p must stay below 2p (acc_reduce + csub)
+        assert t / R_OVER_P + 1 < 2, f"{name}: product bound {t}"
         # 64-bit columns: limbs < 2^26 * sum|c|; 10 terms per column per slot
         worst = max(worst, t)
     return worst
@@ -714,7 +715,7 @@ def check_xround(xr, order):
         assert max(limbs) < 1 << 32, f"{xr.name}: pre-pass limb overflow {key}"
         vbound[X_SCR + i] = (val, limbs)
     for L in xr.lanes:
-        T, cols = 0, [0] * 20
+        T, cols = 0, [0] * 21
         for u, v in L["prod"]:
             (bu, lu), (bv, lv) = src_bound(u), src_bound(v)
             T += bu * bv
@@ -725,13 +726,19 @@ def check_xround(xr, order):
             b, lb = src_bound(src)
             if k < 0:
                 b, lb = 2 * P, NEG_LIMB
-            T += abs(k) * b * (1 << 260)
+            T += abs(k) * b * (1 << R_BITS)
             for i in range(10):
-                cols[10 + i] += abs(k) * lb[i]
-        assert max(cols) < 1 << 64, f"{xr.name}: column overflow"
-        # REDC(T) < T/R + p; fp_reduce8 is exact for inputs below 31 p (q <= 30 keeps
-        # q * p_l inside int32), so T < 800 p^2 (T/R < 28.3 p) leaves a margin
-        assert T < 800 * P * P, f"{xr.name}: REDC input {T / P / P:.1f} p^2"
+                cols[R_BITS // 26 + i] += abs(k) * lb[i]
+        # REDC adds up to 10 digit products (< 2^52 each) and a carry to every column
+        assert max(cols) + 11 * (1 << 52) < 1 << 64, f"{xr.name}: column overflow"
+        # REDC(T) < T/R + p with R = 2^286. Product-only rounds: T < p R gives a result
+        # < 2p (acc_reduce, one conditional subtraction). Rounds with linear terms
+        # (passed through REDC unchanged): result < T/R + p must stay below 31p, the
+        # exact range of fp_reduce8 (q <= 30 keeps q * p_l inside int32).
+        if any(k for _, k in L["lin"]):
+            assert T / (1 << R_BITS) + P < 30 * P, f"{xr.name}: REDC result {T / (1 << R_BITS) / P:.1f} p"
+        else:
+            assert T < P * (1 << R_BITS), f"{xr.name}: REDC input {T / P / P:.1f} p^2"
 
 
 def run_xround(xr, F, A, B):
