@@ -48,6 +48,7 @@ void launch_aggregate(const PointG2* reg, int nreg, const PointG2* blocks, const
                       const AggRequest* reqs, int n, const uint64_t* words, int* order, void* partial_ws,
                       CheckIn* out, int32_t* codes, hipStream_t s);
 size_t agg_partial_bytes();  // workspace bytes per request for launch_aggregate
+size_t agg_fixed_bytes();    // plus this once
 void launch_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst, hipStream_t s);
 void launch_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t* out, hipStream_t s);
 void launch_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, CheckIn* out, hipStream_t s);

@@ -24,7 +24,7 @@ namespace hg {
 //                  all-zero => infinity; else must be on the curve.
 //   cf (cloudflare): each coordinate must be < p; all-zero => infinity; on
 //                  the curve; G2 additionally in the order-n subgroup.
-__global__ void k_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int32_t* codes) {
+__global__ __launch_bounds__(64) void k_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int32_t* codes) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* m = bytes + (size_t)i * 128;
@@ -58,7 +58,7 @@ __global__ void k_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* ou
   codes[i] = code;
 }
 
-__global__ void k_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes) {
+__global__ __launch_bounds__(64) void k_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* m = bytes + (size_t)i * 64;
@@ -80,7 +80,7 @@ __global__ void k_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* ou
 }
 
 // ------------------------------------------------------------------ encode
-__global__ void k_encode_g2(const PointG2* in, int n, uint8_t* out) {
+__global__ __launch_bounds__(64) void k_encode_g2(const PointG2* in, int n, uint8_t* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t* o = out + (size_t)i * 128;
@@ -95,7 +95,7 @@ __global__ void k_encode_g2(const PointG2* in, int n, uint8_t* out) {
   fp_to_be(o + 96, P.y.y);
 }
 
-__global__ void k_encode_g1(const PointG1* in, int n, uint8_t* out) {
+__global__ __launch_bounds__(64) void k_encode_g1(const PointG1* in, int n, uint8_t* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t* o = out + (size_t)i * 64;
@@ -117,7 +117,7 @@ HG_DEV void be32_to_words(uint32_t* w, const uint8_t* b) {
   }
 }
 // pk = k * G2 (G2.ScalarBaseMult)
-__global__ void k_g2_mul_base(const uint8_t* scalars, int n, PointG2* out) {
+__global__ __launch_bounds__(64) void k_g2_mul_base(const uint8_t* scalars, int n, PointG2* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8];
@@ -140,7 +140,7 @@ __global__ void k_g2_mul_base(const uint8_t* scalars, int n, PointG2* out) {
   out[i] = P;
 }
 // sig = k * H (G1.ScalarMult on the hashed message)
-__global__ void k_g1_mul(const PointG1* base, const uint8_t* scalars, int n, PointG1* out) {
+__global__ __launch_bounds__(64) void k_g1_mul(const PointG1* base, const uint8_t* scalars, int n, PointG1* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8];
@@ -164,7 +164,7 @@ __global__ void k_g1_mul(const PointG1* base, const uint8_t* scalars, int n, Poi
 
 // ------------------------------------------------------------------ hash-to-G1
 // H = k * G1 where k is the hashedMessage scalar (validated on the host)
-__global__ void k_hash_point(const uint32_t* k_words, PointG1* out) {
+__global__ __launch_bounds__(64) void k_hash_point(const uint32_t* k_words, PointG1* out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   G1J g;
   const Fp gx = HG_G1X, gy = HG_G1Y;
@@ -182,7 +182,7 @@ __global__ void k_hash_point(const uint32_t* k_words, PointG1* out) {
 // ------------------------------------------------------------------ fixed G2Base lines
 // Same step order as the Miller loop in k_verify: for i = 65..1 a doubling
 // line, then an addition line when NAF[i-1] != 0, then the two Frobenius lines.
-__global__ void k_g2_lines(LineCoef* tab) {
+__global__ __launch_bounds__(64) void k_g2_lines(LineCoef* tab) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int8_t naf[kNafLen] = HG_NAF;
   const Fp2 qx = HG_G2X, qy = HG_G2Y;
@@ -249,7 +249,7 @@ struct BlockIndex {
   int levels;    // highest level with a table
 };
 
-__global__ void k_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst) {
+__global__ __launch_bounds__(64) void k_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= ndst) return;
   const PointG2& a = src[2 * j];
@@ -303,113 +303,147 @@ HG_DEV AggPlan agg_plan(const AggRequest& q, uint32_t cnt, int nreg, int levels)
   return p;
 }
 
-// Longest-processing-time-first order of the requests (one 1024-thread block):
-// a counting sort on the estimated fold cost, so the heaviest requests start
-// first and the light ones fill in behind them.
+// Schedule (one 1024-thread block): the plan of every request, then a counting
+// sort by (lanes L descending, keys to fold descending). k_aggregate packs
+// 64 / L consecutive requests of one bucket into a wave, so small requests
+// share a wave (their folds and log2 L-level trees run side by side) and the
+// heaviest single-request waves start first.
+struct AggSched {
+  int task_start[8];  // first task of lane class c (L = 64 >> c), task_start[7] = total
+  int req_start[8];   // first entry of class c in order[]
+  int nreq[7];
+};
 __global__ __launch_bounds__(1024) void k_agg_order(const AggRequest* reqs, int n, const uint64_t* words,
-                                                    const int32_t* codes, int nreg, int levels, int* order) {
-  __shared__ int hist[64];
-  __shared__ int start[64];
+                                                    const int32_t* codes, int nreg, int levels, int* order,
+                                                    AggPlan* plans, AggSched* sched) {
+  constexpr int kSub = 64;  // cost sub-buckets inside a lane class
+  __shared__ int hist[7 * kSub];
+  __shared__ int start[7 * kSub];
   const int tid = threadIdx.x;
-  if (tid < 64) hist[tid] = 0;
+  for (int i = tid; i < 7 * kSub; i += blockDim.x) hist[i] = 0;
   __syncthreads();
-  auto bucket = [&](int r) -> int {
-    if (codes[r] != HG_OK) return 63;
-    const AggRequest q = reqs[r];
-    uint32_t cnt = 0;
-    for (uint32_t wi = 0; wi < (q.bitlen + 63) / 64; wi++) cnt += __popcll(agg_word(q, words, wi));
-    AggPlan p = agg_plan(q, cnt, nreg, levels);
+  auto key = [&](int r, bool store) -> int {
+    AggPlan p;
+    if (codes[r] != HG_OK) {
+      p.cnt = 0;
+      p.m = 0;
+      p.k = 0;
+      p.lanes = 1;
+      p.comp = false;
+    } else {
+      const AggRequest q = reqs[r];
+      uint32_t cnt = 0;
+      for (uint32_t wi = 0; wi < (q.bitlen + 63) / 64; wi++) cnt += __popcll(agg_word(q, words, wi));
+      p = agg_plan(q, cnt, nreg, levels);
+    }
+    if (store) plans[r] = p;
     int lg = 0;
     while ((1 << lg) < p.lanes) lg++;
-    // fold cost in tenths of a full addition: ceil(m / L) mixed (~0.65) + log2(L) full
-    const int cost = ((int)((p.m + p.lanes - 1) / p.lanes) * 13 + lg * 20) / 4;
-    return 63 - (cost < 63 ? cost : 63);
+    const uint32_t per = (p.m + p.lanes - 1) / p.lanes;  // keys per lane
+    return (6 - lg) * kSub + (kSub - 1 - (int)(per < (uint32_t)(kSub - 1) ? per : kSub - 1));
   };
-  for (int r = tid; r < n; r += blockDim.x) atomicAdd(&hist[bucket(r)], 1);
+  for (int r = tid; r < n; r += blockDim.x) atomicAdd(&hist[key(r, true)], 1);
   __syncthreads();
   if (tid == 0) {
-    int acc = 0;
-    for (int b = 0; b < 64; b++) {
-      start[b] = acc;
-      acc += hist[b];
+    int acc = 0, tasks = 0;
+    for (int c = 0; c < 7; c++) {
+      int nc = 0;
+      sched->req_start[c] = acc;
+      for (int b = c * kSub; b < (c + 1) * kSub; b++) {
+        start[b] = acc;
+        acc += hist[b];
+        nc += hist[b];
+      }
+      sched->nreq[c] = nc;
+      sched->task_start[c] = tasks;
+      const int per_wave = 1 << c;  // requests per wave for L = 64 >> c
+      tasks += (nc + per_wave - 1) / per_wave;
     }
+    sched->req_start[7] = acc;
+    sched->task_start[7] = tasks;
   }
   __syncthreads();
-  for (int r = tid; r < n; r += blockDim.x) order[atomicAdd(&start[bucket(r)], 1)] = r;
+  for (int r = tid; r < n; r += blockDim.x) order[atomicAdd(&start[key(r, false)], 1)] = r;
 }
 
-__global__ __launch_bounds__(64) void k_aggregate(const PointG2* reg, int nreg, BlockIndex bi,
-                                                  const AggRequest* reqs, int n, const uint64_t* words,
-                                                  const int* order, AggPartial* partial, const int32_t* codes) {
+// One wave per task: 64 / L requests of the same lane count L, one group of L
+// lanes each. Per group: compaction of the keys to fold (L words per pass,
+// segmented prefix sums), ceil(m / L) mixed additions per lane, then a
+// log2(L)-level LDS tree; the group root is the request's partial sum.
+__global__ __launch_bounds__(64) void k_aggregate(const PointG2* reg, const AggRequest* reqs,
+                                                  const uint64_t* words, const int* order, const AggPlan* plans,
+                                                  const AggSched* sched, AggPartial* partial) {
   __shared__ G2J part[64];
   __shared__ uint16_t pos[kAggPosCap];
   __shared__ uint32_t cnt_lds[64];
-  if ((int)blockIdx.x >= n) return;
-  const int r = order[blockIdx.x];
-  const AggRequest q = reqs[r];
+  __shared__ uint32_t nw_lds[64];
+  const int t = blockIdx.x;
+  if (t >= sched->task_start[7]) return;  // uniform: fewer tasks than requests
+  int c = 0;
+  while (c < 6 && t >= sched->task_start[c + 1]) c++;
+  const int L = 64 >> c;
   const int lane = threadIdx.x;
-  if (codes[r] != HG_OK) return;  // level error: no aggregate (uniform exit)
-  const uint32_t bitlen = q.bitlen;
-  const uint32_t nwords = (bitlen + 63) / 64;
-  auto word_at = [&](uint32_t wi) -> uint64_t { return agg_word(q, words, wi); };
-  // 1. set count
-  uint32_t c = 0;
-  for (uint32_t wi = lane; wi < nwords; wi += 64) c += __popcll(word_at(wi));
-  cnt_lds[lane] = c;
-  __syncthreads();
-  for (int s2 = 32; s2 > 0; s2 >>= 1) {
-    if (lane < s2) cnt_lds[lane] += cnt_lds[lane + s2];
-    __syncthreads();
+  const int g = lane / L, l = lane % L, gbase = g * L;
+  const int idx = (t - sched->task_start[c]) * (1 << c) + g;
+  const bool has = idx < sched->nreq[c];
+  const int r = has ? order[sched->req_start[c] + idx] : -1;
+  AggRequest q;
+  q.offset = q.bitlen = q.level_size = q.word_offset = 0;
+  AggPlan pl;
+  pl.cnt = pl.m = 0;
+  pl.k = 0;
+  pl.lanes = L;
+  pl.comp = false;
+  if (has) {
+    q = reqs[r];
+    pl = plans[r];
   }
-  const uint32_t cnt = cnt_lds[0];
+  const bool active = has && pl.cnt > 0;  // level errors and empty bitsets fold nothing
+  const uint32_t nwords = active ? (q.bitlen + 63) / 64 : 0;
+  nw_lds[lane] = nwords;
   __syncthreads();
-  const AggPlan plan = agg_plan(q, cnt, nreg, bi.levels);
-  const bool comp = plan.comp;
-  const int k = plan.k, L = plan.lanes;
-  // 2.-3. fold the complement / set keys, 64 words (4096 positions) per pass
+  uint32_t maxw = 0;
+  for (int i = 0; i < 64; i += L) maxw = nw_lds[i] > maxw ? nw_lds[i] : maxw;  // wave-uniform
   G2J acc;
   g2_set_inf(acc);
-  for (uint32_t w0 = 0; w0 < nwords; w0 += 64) {
-    const uint32_t wi = w0 + lane;
+  for (uint32_t w0 = 0; w0 < maxw; w0 += L) {
+    const uint32_t wi = w0 + l;
     uint64_t mb = 0;
     if (wi < nwords) {
-      mb = word_at(wi);
-      if (comp) {
+      mb = agg_word(q, words, wi);
+      if (pl.comp) {
         mb = ~mb;
         const uint32_t lo = wi * 64;
-        if (lo + 64 > bitlen) mb &= (1ull << (bitlen - lo)) - 1;
+        if (lo + 64 > q.bitlen) mb &= (1ull << (q.bitlen - lo)) - 1;
       }
     }
-    // exclusive prefix of per-word counts (Hillis-Steele in LDS)
-    uint32_t pc = __popcll(mb);
+    const uint32_t pc = __popcll(mb);
     cnt_lds[lane] = pc;
     __syncthreads();
-    for (int d = 1; d < 64; d <<= 1) {
-      uint32_t v = lane >= d ? cnt_lds[lane - d] : 0;
+    for (int d = 1; d < L; d <<= 1) {  // inclusive prefix inside the group
+      const uint32_t v = l >= d ? cnt_lds[lane - d] : 0;
       __syncthreads();
       cnt_lds[lane] += v;
       __syncthreads();
     }
-    const uint32_t total = cnt_lds[63];
-    uint32_t at = cnt_lds[lane] - pc;
+    const uint32_t total = cnt_lds[gbase + L - 1];
+    uint32_t at = gbase * 64 + cnt_lds[lane] - pc;  // group region: 64 entries per lane
     while (mb) {
       const int b = __builtin_ctzll(mb);
-      pos[at++] = (uint16_t)(lane * 64 + b);
+      pos[at++] = (uint16_t)(l * 64 + b);
       mb &= mb - 1;
     }
     __syncthreads();
-    if (lane < L) {
-      for (uint32_t t = lane; t < total; t += L) {
-        const PointG2& P = reg[q.offset + w0 * 64 + pos[t]];
-        if (!P.inf) g2_madd(acc, acc, P.x, P.y);
-      }
+    for (uint32_t e = l; e < total; e += L) {
+      const PointG2& P = reg[q.offset + w0 * 64 + pos[gbase * 64 + e]];
+      if (!P.inf) g2_madd(acc, acc, P.x, P.y);
     }
     __syncthreads();
   }
   part[lane] = acc;
   __syncthreads();
   for (int s2 = L / 2; s2 > 0; s2 >>= 1) {
-    if (lane < s2) {
+    if (l < s2) {
       G2J o = part[lane + s2];
       G2J mm = part[lane];
       g2_add(mm, mm, o);
@@ -417,19 +451,18 @@ __global__ __launch_bounds__(64) void k_aggregate(const PointG2* reg, int nreg, 
     }
     __syncthreads();
   }
-  // 4. the root partial; k_agg_finish applies the complement and converts to affine
-  if (lane == 0) {
+  if (has && l == 0) {
     AggPartial& o = partial[r];
-    o.s = part[0];
-    o.cnt = cnt;
-    o.comp = comp ? 1 : 0;
-    o.k = k;
+    o.s = part[lane];
+    o.cnt = pl.cnt;
+    o.comp = pl.comp ? 1 : 0;
+    o.k = pl.k;
   }
 }
 
 // One thread per request: block - fold for complemented requests, affine
 // conversion (Bernstein-Yang inversion), empty-aggregate code.
-__global__ void k_agg_finish(const PointG2* blocks, BlockIndex bi, const AggRequest* reqs, int n,
+__global__ __launch_bounds__(64) void k_agg_finish(const PointG2* blocks, BlockIndex bi, const AggRequest* reqs, int n,
                              const AggPartial* partial, CheckIn* out, int32_t* codes) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n || codes[r] != HG_OK) return;
@@ -459,7 +492,7 @@ __global__ void k_agg_finish(const PointG2* blocks, BlockIndex bi, const AggRequ
 }
 
 // ------------------------------------------------------------------ G1 combine
-__global__ void k_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t* out) {
+__global__ __launch_bounds__(64) void k_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G1J pa, pb, r;
@@ -478,7 +511,7 @@ __global__ void k_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t*
 }
 
 // batched PublicKey.Combine (bn256/go/bn256.go:97-105): out[i] = a[i] + b[i] (G2)
-__global__ void k_g2_combine(const PointG2* a, const PointG2* b, int n, PointG2* out) {
+__global__ __launch_bounds__(64) void k_g2_combine(const PointG2* a, const PointG2* b, int n, PointG2* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G2J pa, pb, r;
@@ -498,24 +531,24 @@ __global__ void k_g2_combine(const PointG2* a, const PointG2* b, int n, PointG2*
 }
 
 // ------------------------------------------------------------------ copy helpers
-__global__ void k_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, CheckIn* out) {
+__global__ __launch_bounds__(64) void k_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, CheckIn* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   out[i].pk = pks[i];
   out[i].sig = sigs[i];
 }
-__global__ void k_merge_codes(const int32_t* a, const int32_t* b, int n, int32_t* out) {
+__global__ __launch_bounds__(64) void k_merge_codes(const int32_t* a, const int32_t* b, int n, int32_t* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // pk decode errors win over sig decode errors (the registry is decoded first)
   out[i] = a[i] != HG_OK ? a[i] : b[i];
 }
-__global__ void k_sig_into_checks(const PointG1* sigs, int n, CheckIn* out) {
+__global__ __launch_bounds__(64) void k_sig_into_checks(const PointG1* sigs, int n, CheckIn* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   out[i].sig = sigs[i];
 }
-__global__ void k_extract_pk(const CheckIn* in, int n, PointG2* out) {
+__global__ __launch_bounds__(64) void k_extract_pk(const CheckIn* in, int n, PointG2* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   out[i] = in[i].pk;
@@ -523,7 +556,7 @@ __global__ void k_extract_pk(const CheckIn* in, int n, PointG2* out) {
 
 // ------------------------------------------------------------------ self test
 // plain-integer words in -> Montgomery product -> plain-integer words out
-__global__ void k_fp_mul(const uint32_t* a, const uint32_t* b, int n, uint32_t* out) {
+__global__ __launch_bounds__(64) void k_fp_mul(const uint32_t* a, const uint32_t* b, int n, uint32_t* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Fp x, y, xm, ym, r, rp;
@@ -570,11 +603,14 @@ void launch_aggregate(const PointG2* reg, int nreg, const PointG2* blocks, const
   bi.levels = levels < 23 ? levels : 23;
   for (int k = 0; k < 24; k++) bi.base[k] = k <= bi.levels ? block_base[k] : 0;
   if (n <= 0) return;
-  k_agg_order<<<1, 1024, 0, s>>>(reqs, n, words, codes, nreg, bi.levels, order);
-  k_aggregate<<<n, 64, 0, s>>>(reg, nreg, bi, reqs, n, words, order, partial, codes);
+  AggPlan* plans = (AggPlan*)((uint8_t*)partial_ws + (size_t)n * sizeof(AggPartial));
+  AggSched* sched = (AggSched*)(plans + n);
+  k_agg_order<<<1, 1024, 0, s>>>(reqs, n, words, codes, nreg, bi.levels, order, plans, sched);
+  k_aggregate<<<n, 64, 0, s>>>(reg, reqs, words, order, plans, sched, partial);
   k_agg_finish<<<nblk(n, 64), 64, 0, s>>>(blocks, bi, reqs, n, partial, out, codes);
 }
-size_t agg_partial_bytes() { return sizeof(AggPartial); }
+size_t agg_partial_bytes() { return sizeof(AggPartial) + sizeof(AggPlan); }
+size_t agg_fixed_bytes() { return sizeof(AggSched); }
 void launch_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst, hipStream_t s) {
   if (ndst > 0) k_block_sums<<<nblk(ndst, 64), 64, 0, s>>>(src, nsrc, dst, ndst);
 }

@@ -420,7 +420,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
                                    bool verify, hipStream_t s) {
   HG_CHECK(c, c->checks.ensure(n));
   HG_CHECK(c, c->order.ensure(n));
-  HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes()));
+  HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
   launch_aggregate(c->reg.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
                    d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
   if (d_agg) {
