@@ -168,29 +168,39 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # HG_BENCH_BACKEND=gloo is a rehearsal mode for boxes with fewer GPUs than
+    # ranks (ranks share devices round-robin, collectives on host copies); the
+    # production path is one rank per GPU over RCCL ("nccl").
+    backend = os.environ.get("HG_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if backend == "gloo" else local
     if dist:
         import torch.distributed as tdist
 
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            tdist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local_dev)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
-    eng = Engine(device=local, flavor="go")
+    eng = Engine(device=local_dev, flavor="go")
     assert eng.set_message(LIB_MESSAGE) == 0
     n = args.batch
     pks, sigs, expect = make_batch(eng, n, seed=1234 + rank)
     d_pks = torch.frombuffer(bytearray(pks), dtype=torch.uint8).to(dev)
     d_sigs = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
     d_codes = torch.zeros(n, dtype=torch.int32, device=dev)
-    gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev) for _ in range(world)]
+    gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev) for _ in range(world)]
     stream = torch.cuda.current_stream(dev)
 
     def step():
         eng.verify_batch_device(d_pks.data_ptr(), d_sigs.data_ptr(), n, d_codes.data_ptr(), stream.cuda_stream)
         # verdict bitset (bit i = check i valid), gathered over RCCL: the only cross-GPU traffic
-        gather_verdicts(pack_verdicts(d_codes), world, gathered)
+        gather_verdicts(pack_verdicts(d_codes).to(coll_dev), world, gathered)
 
     for _ in range(args.warmup):
         step()
@@ -213,7 +223,7 @@ def main():
     kern_ms, launches = eng.timing_read()
     eng.timing_enable(False)
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         dt = float(t.item())
     got = d_codes.cpu().numpy()
@@ -258,7 +268,7 @@ def main():
             tdist.barrier()
         adt = time.perf_counter() - t0
         if dist:
-            t = torch.tensor([adt], dtype=torch.float64, device=dev)
+            t = torch.tensor([adt], dtype=torch.float64, device=coll_dev)
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
             adt = float(t.item())
         assert np.array_equal(d_acodes.cpu().numpy(), aexpect)
