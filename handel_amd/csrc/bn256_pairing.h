@@ -151,32 +151,58 @@ HG_DEV void load_fixed_line(const Team& T, uint32_t* F, const LineCoef* tab, int
   team_sync();
 }
 
-// A point at infinity contributes the unit line (a = b = 0, c = 1): after the
-// G2 program, teams with an infinite pk (sig) overwrite LA, LB, LC (FA, FB,
-// FC); the branch is taken only when some team of the wave needs it.
-HG_DEV void unit_lines(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed) {
-  const bool fix_q = !C.use_q, fix_s = has_fixed && !C.use_s;
-  if (__ballot(fix_q || fix_s) == 0) return;  // wave-uniform
+// A point at infinity contributes the unit line (a = b = 0, c = 1). The
+// G2Base line (FA, FB, FC; FB and FC are evaluated at -sig by the step's first
+// round) is replaced before the round that multiplies it in, the pk line
+// (LA, LB, LC) before x_line_pk; each branch is taken only when some team of
+// the wave needs it. Without a fixed pairing (k_pair) the G2Base line is
+// always the unit line.
+HG_DEV void unit_line_regs(const Team& T, uint32_t* F, bool fix, int ra, int rb, int rc) {
+  if (__ballot(fix) == 0) return;  // wave-uniform
   Fp z, o;
   fp_zero(z);
   fp_one(o);
-  if (T.tl < 6) {
+  if (T.tl < 6 && fix) {
     // element tl of (a.x, a.y, b.x, b.y, c.x, c.y); c.y is the real part of c
     Fp v;
     fp_sel(v, T.tl == 5, o, z);
-    const int fr = T.tl < 2 ? R_FA_x + T.tl : (T.tl < 4 ? R_FB_x + T.tl - 2 : R_FC_x + T.tl - 4);
-    if (fix_q) st_fp(F + (R_LA_x + T.tl) * 10, v);  // LA, LB, LC are consecutive
-    if (fix_s) st_fp(F + fr * 10, v);
+    const int r = T.tl < 2 ? ra + T.tl : (T.tl < 4 ? rb + T.tl - 2 : rc + T.tl - 4);
+    st_fp(F + r * 10, v);
   }
   team_sync();
 }
+HG_DEV void unit_line_fix(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed) {
+  unit_line_regs(T, F, !has_fixed || !C.use_s, R_FA_x, R_FB_x, R_FC_x);
+}
+HG_DEV void unit_line_pk(const Team& T, uint32_t* F, const CheckCtx& C) {
+  unit_line_regs(T, F, !C.use_q, R_LA_x, R_LB_x, R_LC_x);
+}
 
-// f *= pk line (LA, LB, LC) and, when has_fixed, the G2Base line (FA, FB, FC);
-// next: the program that runs after the lines
-HG_DEV void apply_lines(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed, XStream& S, XHint next) {
-  unit_lines(T, F, C, has_fixed);
-  x_line_pk<S_F, S_F>(T, S, has_fixed ? xh<ILineFix<S_F, S_F>>() : next);
-  if (has_fixed) x_line_fix<S_F, S_F>(T, S, next);
+// The Miller loop's fused programs (gen_g2_schedule.py FUSED): a doubling step
+// is MDBL_1 (f^2 beside the doubling's first round), MDBL_2 (f * G2Base line
+// beside its second round) and the pk line; an addition step is PADD_*_1,
+// MADD_*_2 (f * G2Base line beside the second round), PADD_*_3, pk line.
+using IMdbl1 = XInst<XP_MDBL_1, S_F, S_F>;
+using IMdbl2 = XInst<XP_MDBL_2, S_F, S_F>;
+template <int P1, int P2, int P3>
+struct AddStep {
+  using I1 = XInst<P1>;
+  using I2 = XInst<P2, S_F, S_F>;
+  using I3 = XInst<P3>;
+};
+using AddPos = AddStep<XP_PADD_POS_1, XP_MADD_POS_2, XP_PADD_POS_3>;
+using AddNeg = AddStep<XP_PADD_NEG_1, XP_MADD_NEG_2, XP_PADD_NEG_3>;
+using AddF1 = AddStep<XP_PADD_F1_1, XP_MADD_F1_2, XP_PADD_F1_3>;
+using AddF2 = AddStep<XP_PADD_F2_1, XP_MADD_F2_2, XP_PADD_F2_3>;
+
+template <class A>
+HG_DEV void add_step(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed, XStream& S, XHint next) {
+  A::I1::run(T, S, xh<typename A::I2>());
+  unit_line_fix(T, F, C, has_fixed);
+  A::I2::run(T, S, xh<typename A::I3>());
+  A::I3::run(T, S, xh<ILinePk<S_F, S_F>>());
+  unit_line_pk(T, F, C);
+  x_line_pk<S_F, S_F>(T, S, next);
 }
 
 // f = Miller(pk at H) * Miller(G2Base at -sig) (x/crypto optate.go miller, with
@@ -193,30 +219,29 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   for (int i = kNafLen - 1; i > 0; i--) {
     load_fixed_line(T, F, tab, s++);
     DIAG_ADD(0);
-    x_g2<XP_PDBL>(T, S, i != kNafLen - 1 ? xh<ISqr12<S_F, S_F>>() : kLinePk);
+    if (i == kNafLen - 1) XInst<XP_PDBL_1>::run(T, S, xh<IMdbl2>());  // f = 1: no squaring
+    else IMdbl1::run(T, S, xh<IMdbl2>());
     DIAG_ADD(1);
-    if (i != kNafLen - 1) x_sqr12<S_F, S_F>(T, S, kLinePk);
+    unit_line_fix(T, F, C, has_fixed);
+    IMdbl2::run(T, S, kLinePk);
+    unit_line_pk(T, F, C);
     DIAG_ADD(2);
     const int d = naf[i - 1];
-    const XHint step = i > 1 ? xh<IG2<XP_PDBL>>() : xh<IG2<XP_PADD_F1>>();  // after this digit
-    apply_lines(T, F, C, has_fixed, S, d > 0 ? xh<IG2<XP_PADD_POS>>() : d < 0 ? xh<IG2<XP_PADD_NEG>>() : step);
+    const XHint step = i > 1 ? xh<IMdbl1>() : xh<AddF1::I1>();  // after this digit
+    x_line_pk<S_F, S_F>(T, S, d > 0 ? xh<AddPos::I1>() : d < 0 ? xh<AddNeg::I1>() : step);
     DIAG_ADD(3);
     if (d != 0) {
       load_fixed_line(T, F, tab, s++);
       DIAG_ADD(0);
-      if (d > 0) x_g2<XP_PADD_POS>(T, S, kLinePk);
-      else x_g2<XP_PADD_NEG>(T, S, kLinePk);
+      if (d > 0) add_step<AddPos>(T, F, C, has_fixed, S, step);
+      else add_step<AddNeg>(T, F, C, has_fixed, S, step);
       DIAG_ADD(4);
-      apply_lines(T, F, C, has_fixed, S, step);
-      DIAG_ADD(3);
     }
   }
   load_fixed_line(T, F, tab, s++);
-  x_g2<XP_PADD_F1>(T, S, kLinePk);
-  apply_lines(T, F, C, has_fixed, S, xh<IG2<XP_PADD_F2>>());
+  add_step<AddF1>(T, F, C, has_fixed, S, xh<AddF2::I1>());
   load_fixed_line(T, F, tab, s++);
-  x_g2<XP_PADD_F2>(T, S, kLinePk);
-  apply_lines(T, F, C, has_fixed, S, after);
+  add_step<AddF2>(T, F, C, has_fixed, S, after);
 }
 
 HG_DEV uint32_t* team_regs(const Team& T) { return T.base + kSlots * kFp12Words; }

@@ -40,7 +40,7 @@ struct XHint {
   int off, w;  // table offset and per-lane stride of the round to prefetch (off < 0: none)
 };
 struct XStream;
-template <int NV, int NT, int NP, int NL, int W, int OFF>
+template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2>
 HG_DEV void x_round(const Team& T, XStream& S, XHint nxt);
 
 }  // namespace hg
@@ -124,9 +124,35 @@ HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t 
   for (int l = 0; l < 10; l++) out[l] = (uint32_t)acc[l] + (uint32_t)negk * kP2N[l];
 }
 
+// One job: sum of NP products of LDS operands plus NL R-shifted linear terms,
+// reduced once. Entries from `base`: NP x (u, v), NL x term, dst.
+template <int W, int NP, int NL>
+HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst) {
+  Acc acc;
+  acc_zero(acc);
+  x_for<NP>([&](auto p) {
+    Fp a, b;
+    ld_fp(a, x_at(T, x_off(w, base + 2 * p)));
+    ld_fp(b, x_at(T, x_off(w, base + 2 * p + 1)));
+    acc_mad(acc, a, b);
+  });
+  constexpr int lbase = 2 * NP;
+  if constexpr (NL > 0) {
+    uint32_t val[10];
+    x_lincomb<W, NL>(T, w, base + lbase, val);
+#pragma unroll
+    for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] += val[l];
+  }
+  dst = x_off(w, base + lbase + NL);
+  if constexpr (NL > 0) acc_reduce_wide(r, acc);  // linear terms: result < 31p
+  else acc_reduce(r, acc);                        // products only: < 2p, one subtraction
+}
+
 // One round. Table layout per lane (16-bit entries): NV x (dst, NT x term),
-// NP x (u, v), NL x term, dst; padded to W dwords.
-template <int NV, int NT, int NP, int NL, int W, int OFF>
+// then job 1 (NP x (u, v), NL x term, dst) and, in a fused round (NP2 + NL2 >
+// 0), job 2 (NP2 x (u, v), NL2 x term, dst2); padded to W dwords. Both jobs
+// read before either result is stored, so in-place programs are fine.
+template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2>
 HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
   if (S.off != OFF) x_fetch(T, S, XHint{OFF, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
@@ -146,28 +172,21 @@ HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
     });
     team_sync();
   }
-  constexpr int pbase = NV * (1 + NT);
-  Acc acc;
-  acc_zero(acc);
-  x_for<NP>([&](auto p) {
-    Fp a, b;
-    ld_fp(a, x_at(T, x_off(w, pbase + 2 * p)));
-    ld_fp(b, x_at(T, x_off(w, pbase + 2 * p + 1)));
-    acc_mad(acc, a, b);
-  });
-  constexpr int lbase = pbase + 2 * NP;
-  if constexpr (NL > 0) {
-    uint32_t val[10];
-    x_lincomb<W, NL>(T, w, lbase, val);
-#pragma unroll
-    for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] += val[l];
-  }
-  const uint32_t dst = x_off(w, lbase + NL);
+  constexpr int jbase = NV * (1 + NT);
   Fp r;
-  if constexpr (NL > 0) acc_reduce_wide(r, acc);  // linear terms: result < 31p
-  else acc_reduce(r, acc);                        // products only: < 2p, one subtraction
-  team_sync();
-  if (dst != 0xffffu) st_fp(x_at(T, dst), r);
+  uint32_t dst;
+  x_job<W, NP, NL>(T, w, jbase, r, dst);
+  if constexpr (NP2 > 0 || NL2 > 0) {
+    Fp r2;
+    uint32_t dst2;
+    x_job<W, NP2, NL2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
+    team_sync();
+    if (dst != 0xffffu) st_fp(x_at(T, dst), r);
+    if (dst2 != 0xffffu) st_fp(x_at(T, dst2), r2);
+  } else {
+    team_sync();
+    if (dst != 0xffffu) st_fp(x_at(T, dst), r);
+  }
   team_sync();
 }
 

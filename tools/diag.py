@@ -22,7 +22,7 @@ import numpy as np  # noqa: E402
 import bench  # noqa: E402
 from handel_amd.engine import Engine  # noqa: E402
 
-NAMES = ["fixed_line_load", "g2_double", "fp12_square", "line_mul", "g2_add", "fe_inversion", "fe_rest",
+NAMES = ["fixed_line_load", "mdbl1_sqr_and_dbl_r1", "mdbl2_fixline_and_dbl_r2", "pk_line_mul", "add_step", "fe_inversion", "fe_rest",
          "fe_pow_u_x3", "miller_total", "final_exp_total", "kernel_total"]
 
 

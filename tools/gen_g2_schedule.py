@@ -598,11 +598,21 @@ def _xsrc(r):
 
 
 class XRound:
-    def __init__(self, nv, nt, np_, nl, lanes, name):
+    """A compiled round. Each lane runs one job (prod, lin -> dst) or, in a
+    fused round, a second independent job (prod2, lin2 -> dst2) after the
+    first: two programs' rounds share one pre-pass, table fetch and sync."""
+    def __init__(self, nv, nt, np_, nl, lanes, name, np2=0, nl2=0):
         self.nv, self.nt, self.np, self.nl, self.lanes, self.name = nv, nt, np_, nl, lanes, name
+        self.np2, self.nl2 = np2, nl2
+
+    @property
+    def fused(self):
+        return self.np2 > 0 or self.nl2 > 0
 
     def words(self):
         nhalves = self.nv * (1 + self.nt) + 2 * self.np + self.nl + 1
+        if self.fused:
+            nhalves += 2 * self.np2 + self.nl2 + 1
         return (nhalves + 1) // 2
 
     def lane_halves(self, t):
@@ -621,6 +631,12 @@ class XRound:
         for src, c in L["lin"]:
             h.append((src << 8) | (c & 255))
         h.append(off(L["dst"]))
+        if self.fused:
+            for u, v in L["prod2"]:
+                h += [off(u), off(v)]
+            for src, c in L["lin2"]:
+                h.append((src << 8) | (c & 255))
+            h.append(off(L["dst2"]))
         h += [0] * (2 * self.words() - len(h))
         return h
 
@@ -640,7 +656,7 @@ class XRound:
         return b
 
 
-def compile_round(lanes, name, scratch_cap):
+def compile_round(lanes, name, scratch_cap, lanes2=None):
     one_lc = [(REG["ONE"], 1)]
     values = {}      # canonical lincomb -> scratch code
     order = []
@@ -655,24 +671,38 @@ def compile_round(lanes, name, scratch_cap):
             order.append(key)
         return values[key]
 
-    per_lane = []
-    for l in lanes:
-        prods, lins = [], []
-        for a, b in l.slots:
-            if list(b) == one_lc:
-                lins += [(_xsrc(r), k) for r, k in a if k != 0]
-            elif list(a) == one_lc:
-                lins += [(_xsrc(r), k) for r, k in b if k != 0]
-            else:
-                prods.append((operand(a), operand(b)))
-        per_lane.append((l.dst, prods, lins))
-    assert len(per_lane) <= 16, name
+    def jobs(ls):
+        per = []
+        for l in ls:
+            prods, lins = [], []
+            for a, b in l.slots:
+                if list(b) == one_lc:
+                    lins += [(_xsrc(r), k) for r, k in a if k != 0]
+                elif list(a) == one_lc:
+                    lins += [(_xsrc(r), k) for r, k in b if k != 0]
+                else:
+                    prods.append((operand(a), operand(b)))
+            per.append((l.dst, prods, lins))
+        assert len(per) <= 16, name
+        return per
+
+    per_lane = jobs(lanes)
+    per_lane2 = jobs(lanes2) if lanes2 is not None else []
+    if lanes2 is not None:
+        # the first job's destinations are written after the second job reads: no overlap
+        d1 = {d for d, _, _ in per_lane}
+        for _, p2, l2 in per_lane2:
+            assert not ({u for u, v in p2} | {v for u, v in p2} | {s for s, _ in l2}) & d1, name
     nvals = len(order)
     assert nvals <= scratch_cap, f"{name}: {nvals} pre-pass values > scratch {scratch_cap}"
     nv = (nvals + 15) // 16
     nt = max([len(k) for k in order] or [0])
     np_ = max(len(p) for _, p, _ in per_lane)
     nl = max(len(q) for _, _, q in per_lane)
+    np2 = max([len(p) for _, p, _ in per_lane2] or [0])
+    nl2 = max([len(q) for _, _, q in per_lane2] or [0])
+    if lanes2 is not None and np2 == 0 and nl2 == 0:
+        nl2 = 1  # keep the fused layout
     zero = REG["ZERO"]
     out = []
     for t in range(16):
@@ -684,14 +714,17 @@ def compile_round(lanes, name, scratch_cap):
                 pre.append((X_SCR + vi, terms))
             else:
                 pre.append((NONE, [(zero, 0)] * nt))
-        if t < len(per_lane):
-            dst, prods, lins = per_lane[t]
-        else:
-            dst, prods, lins = NONE, [], []
+        dst, prods, lins = per_lane[t] if t < len(per_lane) else (NONE, [], [])
         prods = prods + [(zero, zero)] * (np_ - len(prods))
         lins = lins + [(zero, 0)] * (nl - len(lins))
-        out.append({"pre": pre, "prod": prods, "lin": lins, "dst": dst})
-    xr = XRound(nv, nt, np_, nl, out, name)
+        L = {"pre": pre, "prod": prods, "lin": lins, "dst": dst}
+        if lanes2 is not None:
+            dst2, prods2, lins2 = per_lane2[t] if t < len(per_lane2) else (NONE, [], [])
+            L["prod2"] = prods2 + [(zero, zero)] * (np2 - len(prods2))
+            L["lin2"] = lins2 + [(zero, 0)] * (nl2 - len(lins2))
+            L["dst2"] = dst2
+        out.append(L)
+    xr = XRound(nv, nt, np_, nl, out, name, np2, nl2)
     check_xround(xr, order)
     return xr
 
@@ -714,7 +747,11 @@ def check_xround(xr, order):
             limbs = [a + abs(k) * b for a, b in zip(limbs, lb)]
         assert max(limbs) < 1 << 32, f"{xr.name}: pre-pass limb overflow {key}"
         vbound[X_SCR + i] = (val, limbs)
-    for L in xr.lanes:
+    jobs = [(L["prod"], L["lin"]) for L in xr.lanes]
+    if xr.fused:
+        jobs += [(L["prod2"], L["lin2"]) for L in xr.lanes]
+    for prod, lin in jobs:
+        L = {"prod": prod, "lin": lin}
         T, cols = 0, [0] * 21
         for u, v in L["prod"]:
             (bu, lu), (bv, lv) = src_bound(u), src_bound(v)
@@ -760,24 +797,60 @@ def run_xround(xr, F, A, B):
                 S[dst] = sum(k * get(src) for src, k in terms) % P
     out = {}
     for L in xr.lanes:
-        if L["dst"] == NONE:
-            continue
-        acc = sum(get(u) * get(v) for u, v in L["prod"]) + sum(k * get(src) for src, k in L["lin"])
-        out[L["dst"]] = acc % P
+        for pk, lk, dk in (("prod", "lin", "dst"), ("prod2", "lin2", "dst2")):
+            if dk not in L or L[dk] == NONE:
+                continue
+            acc = sum(get(u) * get(v) for u, v in L[pk]) + sum(k * get(src) for src, k in L[lk])
+            assert L[dk] not in out, "two jobs write one destination"
+            out[L[dk]] = acc % P
     return out
 
 
 X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
-SCRATCH_CAP = {"FE": 96, "ML": 48}
+SCRATCH_CAP = {"FE": 96, "ML": 96}  # ML: slots C..L are free during the Miller loop
 X_PROGRAMS = {  # name -> (program, scratch context)
     "PDBL": "ML", "PADD_POS": "ML", "PADD_NEG": "ML", "PADD_F1": "ML", "PADD_F2": "ML",
+    "MDBL_1": "ML", "MDBL_2": "ML", "PDBL_1": "ML",
+    "PADD_POS_1": "ML", "MADD_POS_2": "ML", "PADD_POS_3": "ML", "PADD_NEG_1": "ML", "MADD_NEG_2": "ML",
+    "PADD_NEG_3": "ML", "PADD_F1_1": "ML", "MADD_F1_2": "ML", "PADD_F1_3": "ML", "PADD_F2_1": "ML",
+    "MADD_F2_2": "ML", "PADD_F2_3": "ML",
     "SQR12": "ML", "LINE_PK": "ML", "LINE_FIX": "ML", "CYC_SQR": "FE", "MUL12": "FE", "CYC_SQR_X": "FE",
 }
 
 
+# Miller-loop programs whose rounds fuse two independent rounds (see XRound):
+# name -> list of rounds, each (program, round) or ((program, round), (program, round)).
+FUSED = {
+    "MDBL_1": [(("SQR12", 0), ("PDBL", 0))],          # f^2 beside the doubling's first round
+    "MDBL_2": [(("LINE_FIX", 0), ("PDBL", 1))],       # f * G2Base line beside its second round
+    "PDBL_1": [("PDBL", 0)],                          # first iteration (f = 1: no squaring)
+}
+for _v in ("POS", "NEG", "F1", "F2"):
+    FUSED[f"PADD_{_v}_1"] = [(f"PADD_{_v}", 0)]
+    FUSED[f"MADD_{_v}_2"] = [(("LINE_FIX", 0), (f"PADD_{_v}", 1))]
+    FUSED[f"PADD_{_v}_3"] = [(f"PADD_{_v}", 2)]
+
+
+def _compile_fused(name, ctx):
+    out = []
+    for i, spec in enumerate(FUSED[name]):
+        if isinstance(spec[0], tuple):
+            (p1, r1), (p2, r2) = spec
+            out.append(compile_round(PROGRAMS[p1][r1], f"{name}[{i}]", SCRATCH_CAP[ctx], PROGRAMS[p2][r2]))
+        else:
+            p1, r1 = spec
+            out.append(compile_round(PROGRAMS[p1][r1], f"{name}[{i}]", SCRATCH_CAP[ctx]))
+    return out
+
+
 def compile_all():
-    return {name: [compile_round(r, f"{name}[{i}]", SCRATCH_CAP[ctx]) for i, r in enumerate(PROGRAMS[name])]
-            for name, ctx in X_PROGRAMS.items()}
+    X = {}
+    for name, ctx in X_PROGRAMS.items():
+        if name in FUSED:
+            X[name] = _compile_fused(name, ctx)
+        else:
+            X[name] = [compile_round(r, f"{name}[{i}]", SCRATCH_CAP[ctx]) for i, r in enumerate(PROGRAMS[name])]
+    return X
 
 
 def run_xprogram(rounds, F, A=None, B=None):
@@ -850,12 +923,41 @@ def validate_x(seed=2):
         G = dict(F)
         run_xprogram(X["PDBL"], G)
         check_proj(G, r_new, (a, b, c), "xPDBL")
+        # fused Miller-loop programs: f^2 and the G2Base line beside the G2 step rounds
+        f0 = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
+        flat0 = [z for pair in f0 for z in pair]
+        fl_a, fl_bx, fl_cy = (rng.randrange(P), rng.randrange(P)), (rng.randrange(P), rng.randrange(P)), \
+            (rng.randrange(P), rng.randrange(P))
+        F[REG["SX"]], F[REG["NSY"]] = rng.randrange(P), rng.randrange(P)
+        put(F, "FA", fl_a)
+        put(F, "FBX", fl_bx)
+        put(F, "FCY", fl_cy)
+        fix = (fl_a, O.f2_mul(fl_bx, (0, F[REG["SX"]])), O.f2_mul(fl_cy, (0, F[REG["NSY"]])))
+        unfl = lambda D: [(D[2 * k], D[2 * k + 1]) for k in range(6)]  # noqa: E731
+        G = dict(F)
+        sq = run_xprogram(X["MDBL_1"], G, flat0)
+        assert unfl(sq) == O.f12_sqr(f0), "xMDBL_1 square"
+        d2 = run_xprogram(X["MDBL_2"], G, [sq[e] for e in range(12)])
+        assert unfl(d2) == O._mul_line(O.f12_sqr(f0), *fix), "xMDBL_2 fixed line"
+        check_proj(G, r_new, (a, b, c), "xMDBL")
+        G = dict(F)
+        run_xprogram(X["PDBL_1"], G)
+        d2 = run_xprogram(X["MDBL_2"], G, flat0)
+        assert unfl(d2) == O._mul_line(f0, *fix), "xPDBL_1/MDBL_2 fixed line"
+        check_proj(G, r_new, (a, b, c), "xPDBL_1")
         for prog, pq in (("PADD_POS", (Q[0], Q[1])), ("PADD_NEG", (Q[0], O.f2_neg(Q[1]))),
                          ("PADD_F1", (getf(F, "P1X"), getf(F, "P1Y")))):
             a, b, c, r_new = O._line_add(r, pq, *Hp, O.f2_sqr(pq[1]))
             G = dict(F)
             run_xprogram(X[prog], G)
             check_proj(G, r_new, (a, b, c), "x" + prog)
+            v = prog[5:]
+            G = dict(F)
+            run_xprogram(X[f"PADD_{v}_1"], G)
+            d2 = run_xprogram(X[f"MADD_{v}_2"], G, flat0)
+            run_xprogram(X[f"PADD_{v}_3"], G)
+            assert unfl(d2) == O._mul_line(f0, *fix), "xMADD fixed line"
+            check_proj(G, r_new, (a, b, c), "x" + prog + " split")
         f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
         g = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
         flat = lambda v: [z for pair in v for z in pair]  # noqa: E731
@@ -902,7 +1004,10 @@ INSTANCES = sorted(set(
     + [("SQR12", ("F", "F")), ("SQR12", ("F", "A")), ("LINE_PK", ("F", "F")), ("LINE_FIX", ("F", "F"))]
     # tools/opcycles.hip
     + [("CYC_SQR_X", ("A", "A")), ("SQR12", ("A", "A")), ("LINE_PK", ("A", "A"))]
-    + [(g, ()) for g in ("PDBL", "PADD_POS", "PADD_NEG", "PADD_F1", "PADD_F2")]))
+    + [(g, ()) for g in ("PDBL", "PADD_POS", "PADD_NEG", "PADD_F1", "PADD_F2", "PDBL_1")]
+    + [(f"PADD_{v}_{i}", ()) for v in ("POS", "NEG", "F1", "F2") for i in (1, 3)]
+    + [(f"MADD_{v}_2", ("F", "F")) for v in ("POS", "NEG", "F1", "F2")]
+    + [("MDBL_1", ("F", "F")), ("MDBL_2", ("F", "F"))]))
 
 
 def bind(xr, binding, ctx):
@@ -931,13 +1036,18 @@ def bind(xr, binding, ctx):
 
     lanes = []
     for L in xr.lanes:
-        lanes.append({"pre": [(NONE if d == NONE else src(d), [(src(s), c) for s, c in t]) for d, t in L["pre"]],
-                      "prod": [(src(u), src(v)) for u, v in L["prod"]],
-                      "lin": [(src(s), c) for s, c in L["lin"]], "dst": dst(L["dst"])})
+        b = {"pre": [(NONE if d == NONE else src(d), [(src(s), c) for s, c in t]) for d, t in L["pre"]],
+             "prod": [(src(u), src(v)) for u, v in L["prod"]],
+             "lin": [(src(s), c) for s, c in L["lin"]], "dst": dst(L["dst"])}
+        if xr.fused:
+            b["prod2"] = [(src(u), src(v)) for u, v in L["prod2"]]
+            b["lin2"] = [(src(s), c) for s, c in L["lin2"]]
+            b["dst2"] = dst(L["dst2"])
+        lanes.append(b)
     for L in lanes:
-        for v in [L["dst"]] + [d for d, _ in L["pre"]]:
+        for v in [L["dst"], L.get("dst2", NONE)] + [d for d, _ in L["pre"]]:
             assert v == NONE or v < F_BASE + NREGS, "index out of the team region"
-    out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name)
+    out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     return out
 
 
@@ -950,9 +1060,10 @@ def run_bound(rounds, mem):
                     mem[d] = sum(k * mem[s] for s, k in terms) % P
         out = {}
         for L in xr.lanes:
-            if L["dst"] != NONE:
-                out[L["dst"]] = (sum(mem[u] * mem[v] for u, v in L["prod"])
-                                 + sum(k * mem[s] for s, k in L["lin"])) % P
+            for pk, lk, dk in (("prod", "lin", "dst"), ("prod2", "lin2", "dst2")):
+                if dk in L and L[dk] != NONE:
+                    out[L[dk]] = (sum(mem[u] * mem[v] for u, v in L[pk])
+                                  + sum(k * mem[s] for s, k in L[lk])) % P
         for d, v in out.items():
             mem[d] = v
 
@@ -1007,7 +1118,8 @@ def emit_x(X, path):
         for i, (bx, off) in enumerate(rounds):
             # each round prefetches the next round's words (the last one: the caller's hint)
             nxt = f"XHint{{{rounds[i + 1][1]}, {rounds[i + 1][0].words()}}}" if i + 1 < len(rounds) else "h"
-            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {off}>(T, S, {nxt});")
+            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {off}, {bx.np2}, {bx.nl2}>"
+                         f"(T, S, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
