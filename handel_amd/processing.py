@@ -12,12 +12,12 @@ function of (msg, range, bitset, sig), so batching cannot change them.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import partitioner as part
-from ._lib import HG_OK
+from ._lib import HG_ERR_SIG_UNMARSHAL, HG_OK
 from .engine import REQ_DTYPE, Engine
 
 
@@ -76,6 +76,29 @@ class BatchVerifier:
                 out.append(None)
             else:
                 out.append("handel: " + self.eng.code_string(int(c)))
+        return out
+
+    def verify_packets(self, packets: Sequence[Tuple[int, bytes]]) -> List[Optional[str]]:
+        """Packet-level batch: for each (level, MultiSig
+        bytes) as handel.go:390-436 receives them, MultiSignature.Unmarshal
+        (crypto.go:86-110: u16 length, WilffBitSet blob, 64-byte signature) on
+        the host, then verifySignature for every well-formed packet in one GPU
+        batch. Returns None or the error text the reference would log."""
+        out: List[Optional[str]] = [None] * len(packets)
+        todo, where = [], []
+        for i, (level, buf) in enumerate(packets):
+            try:
+                bits, sig = part.multisig_unmarshal(buf)
+            except ValueError as e:
+                out[i] = str(e)
+                continue
+            if len(sig) != 64:  # x/crypto G1.Unmarshal wants exactly 64 bytes
+                out[i] = self.eng.code_string(HG_ERR_SIG_UNMARSHAL)
+                continue
+            todo.append(IncomingSig(0, level, bits, sig))
+            where.append(i)
+        for i, e in zip(where, self.verify_levels(todo) if todo else []):
+            out[i] = e
         return out
 
     def verify_ranges(self, items) -> np.ndarray:
