@@ -40,7 +40,7 @@ struct XHint {
   int off, w;  // table offset and per-lane stride of the round to prefetch (off < 0: none)
 };
 struct XStream;
-template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2>
+template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2, int KP, int KL1, int KL2>
 HG_DEV void x_round(const Team& T, XStream& S, XHint nxt);
 
 }  // namespace hg
@@ -103,30 +103,34 @@ HG_DEV uint32_t* x_at(const Team& T, uint32_t byte_off) {
   return (uint32_t*)__builtin_assume_aligned((uint8_t*)T.base + byte_off, 8);
 }
 
-// Evaluates sum_t c_t * x_t (+ K (2p)'' with K = sum of |c_t| over the negative
-// c_t, so every limb is a non-negative exact sum) into acc[10] as 32-bit limbs:
-// one v_mad_i64_i32 per limb and term, the correction once per value.
-template <int W, int NT>
+// Evaluates sum_t c_t * x_t + K (2p)'' into out[10] as 32-bit limbs, where K
+// (a round constant from the generator) is at least the sum of |c_t| over the
+// negative c_t of every lane's combination, so every limb is a non-negative
+// exact sum: one 32-bit multiply-add per limb and term, the correction folded
+// into constants.
+// K < 0: the correction is each lane's own sum of negative coefficients (a
+// runtime multiply), for rounds where a uniform K would overflow a bound.
+template <int W, int NT, int K>
 HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t (&out)[10]) {
-  int64_t acc[10];
+  uint32_t acc[10];
 #pragma unroll
-  for (int l = 0; l < 10; l++) acc[l] = 0;
-  int32_t negk = 0;
+  for (int l = 0; l < 10; l++) acc[l] = K >= 0 ? (uint32_t)K * kP2N[l] : 0u;
+  uint32_t negk = 0;
   x_for<NT>([&](auto t) {
     const uint32_t off = x_term_off(w, base + t);
     const int32_t c = x_coef(w, base + t);
     const uint32_t* x = x_at(T, off);
-    negk += c < 0 ? -c : 0;
+    if constexpr (K < 0) negk += c < 0 ? (uint32_t)-c : 0u;
 #pragma unroll
-    for (int l = 0; l < 10; l++) acc[l] += (int64_t)c * (int32_t)x[l];
+    for (int l = 0; l < 10; l++) acc[l] += (uint32_t)c * x[l];
   });
 #pragma unroll
-  for (int l = 0; l < 10; l++) out[l] = (uint32_t)acc[l] + (uint32_t)negk * kP2N[l];
+  for (int l = 0; l < 10; l++) out[l] = K >= 0 ? acc[l] : acc[l] + negk * kP2N[l];
 }
 
 // One job: sum of NP products of LDS operands plus NL R-shifted linear terms,
 // reduced once. Entries from `base`: NP x (u, v), NL x term, dst.
-template <int W, int NP, int NL>
+template <int W, int NP, int NL, int KL>
 HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst) {
   Acc acc;
   acc_zero(acc);
@@ -139,7 +143,7 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
   constexpr int lbase = 2 * NP;
   if constexpr (NL > 0) {
     uint32_t val[10];
-    x_lincomb<W, NL>(T, w, base + lbase, val);
+    x_lincomb<W, NL, KL>(T, w, base + lbase, val);
 #pragma unroll
     for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] += val[l];
   }
@@ -152,7 +156,7 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 // then job 1 (NP x (u, v), NL x term, dst) and, in a fused round (NP2 + NL2 >
 // 0), job 2 (NP2 x (u, v), NL2 x term, dst2); padded to W dwords. Both jobs
 // read before either result is stored, so in-place programs are fine.
-template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2>
+template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2, int KP, int KL1, int KL2>
 HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
   if (S.off != OFF) x_fetch(T, S, XHint{OFF, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
@@ -163,7 +167,7 @@ HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
       constexpr int base = v * (1 + NT);
       const uint32_t dst = x_off(w, base);
       uint32_t val[10];
-      x_lincomb<W, NT>(T, w, base + 1, val);
+      x_lincomb<W, NT, KP>(T, w, base + 1, val);
       if (dst != 0xffffu) {
         uint32_t* o = x_at(T, dst);
 #pragma unroll
@@ -175,11 +179,11 @@ HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
   constexpr int jbase = NV * (1 + NT);
   Fp r;
   uint32_t dst;
-  x_job<W, NP, NL>(T, w, jbase, r, dst);
+  x_job<W, NP, NL, KL1>(T, w, jbase, r, dst);
   if constexpr (NP2 > 0 || NL2 > 0) {
     Fp r2;
     uint32_t dst2;
-    x_job<W, NP2, NL2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
+    x_job<W, NP2, NL2, KL2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
     team_sync();
     if (dst != 0xffffu) st_fp(x_at(T, dst), r);
     if (dst2 != 0xffffu) st_fp(x_at(T, dst2), r2);

@@ -605,6 +605,12 @@ class XRound:
         self.nv, self.nt, self.np, self.nl, self.lanes, self.name = nv, nt, np_, nl, lanes, name
         self.np2, self.nl2 = np2, nl2
 
+        def negk(terms):
+            return sum(-k for _, k in terms if k < 0)
+        self.kp = max([negk(t) for L in lanes for d, t in L["pre"] if d != NONE] or [0])
+        self.kl1 = max([negk(L["lin"]) for L in lanes] or [0])
+        self.kl2 = max([negk(L.get("lin2", [])) for L in lanes] or [0])
+
     @property
     def fused(self):
         return self.np2 > 0 or self.nl2 > 0
@@ -725,7 +731,12 @@ def compile_round(lanes, name, scratch_cap, lanes2=None):
             L["dst2"] = dst2
         out.append(L)
     xr = XRound(nv, nt, np_, nl, out, name, np2, nl2)
-    check_xround(xr, order)
+    try:
+        check_xround(xr, order)
+    except AssertionError:
+        # the round-uniform correction overflows a bound: per-lane corrections
+        xr.kp = xr.kl1 = xr.kl2 = -1
+        check_xround(xr, order)
     return xr
 
 
@@ -736,22 +747,27 @@ def check_xround(xr, order):
             return vbound[code]
         return (P, CANON_LIMB)
 
+    # Every value of the pre-pass (and every lane's linear terms of a job) adds the
+    # round-uniform correction K (2p)'' with K = the largest sum of negative
+    # coefficients (xr.kp / kl1 / kl2): a compile-time constant in the executor.
     vbound = {}
     for i, key in enumerate(order):
-        val, limbs = 0, [0] * 10
+        kp = xr.kp if xr.kp >= 0 else sum(-k for _, k in key if k < 0)  # -1: per-lane correction
+        val, limbs = kp * 2 * P, [kp * x for x in P2N]
         for src, k in key:
-            v, lb = src_bound(src)
-            if k < 0:
-                v, lb = 2 * P, NEG_LIMB
-            val += abs(k) * v
-            limbs = [a + abs(k) * b for a, b in zip(limbs, lb)]
+            if k > 0:
+                v, lb = src_bound(src)
+                val += k * v
+                limbs = [a + k * b for a, b in zip(limbs, lb)]
         assert max(limbs) < 1 << 32, f"{xr.name}: pre-pass limb overflow {key}"
         vbound[X_SCR + i] = (val, limbs)
-    jobs = [(L["prod"], L["lin"]) for L in xr.lanes]
+    jobs = [(L["prod"], L["lin"], xr.kl1, xr.nl) for L in xr.lanes]
     if xr.fused:
-        jobs += [(L["prod2"], L["lin2"]) for L in xr.lanes]
-    for prod, lin in jobs:
+        jobs += [(L["prod2"], L["lin2"], xr.kl2, xr.nl2) for L in xr.lanes]
+    for prod, lin, kl, nl in jobs:
         L = {"prod": prod, "lin": lin}
+        if kl < 0:
+            kl = sum(-k for _, k in lin if k < 0)
         T, cols = 0, [0] * 21
         for u, v in L["prod"]:
             (bu, lu), (bv, lv) = src_bound(u), src_bound(v)
@@ -759,20 +775,24 @@ def check_xround(xr, order):
             for i in range(10):
                 for j in range(10):
                     cols[i + j] += lu[i] * lv[j]
-        for src, k in L["lin"]:
-            b, lb = src_bound(src)
-            if k < 0:
-                b, lb = 2 * P, NEG_LIMB
-            T += abs(k) * b * (1 << R_BITS)
+        if nl > 0:
+            T += kl * 2 * P * (1 << R_BITS)
             for i in range(10):
-                cols[R_BITS // 26 + i] += abs(k) * lb[i]
+                cols[R_BITS // 26 + i] += kl * P2N[i]
+        for src, k in L["lin"]:
+            if k <= 0:
+                continue
+            b, lb = src_bound(src)
+            T += k * b * (1 << R_BITS)
+            for i in range(10):
+                cols[R_BITS // 26 + i] += k * lb[i]
         # REDC adds up to 10 digit products (< 2^52 each) and a carry to every column
         assert max(cols) + 11 * (1 << 52) < 1 << 64, f"{xr.name}: column overflow"
         # REDC(T) < T/R + p with R = 2^286. Product-only rounds: T < p R gives a result
         # < 2p (acc_reduce, one conditional subtraction). Rounds with linear terms
         # (passed through REDC unchanged): result < T/R + p must stay below 31p, the
         # exact range of fp_reduce8 (q <= 30 keeps q * p_l inside int32).
-        if any(k for _, k in L["lin"]):
+        if nl > 0:
             assert T / (1 << R_BITS) + P < 30 * P, f"{xr.name}: REDC result {T / (1 << R_BITS) / P:.1f} p"
         else:
             assert T < P * (1 << R_BITS), f"{xr.name}: REDC input {T / P / P:.1f} p^2"
@@ -1048,6 +1068,7 @@ def bind(xr, binding, ctx):
         for v in [L["dst"], L.get("dst2", NONE)] + [d for d, _ in L["pre"]]:
             assert v == NONE or v < F_BASE + NREGS, "index out of the team region"
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
+    out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
     return out
 
 
@@ -1118,8 +1139,8 @@ def emit_x(X, path):
         for i, (bx, off) in enumerate(rounds):
             # each round prefetches the next round's words (the last one: the caller's hint)
             nxt = f"XHint{{{rounds[i + 1][1]}, {rounds[i + 1][0].words()}}}" if i + 1 < len(rounds) else "h"
-            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {off}, {bx.np2}, {bx.nl2}>"
-                         f"(T, S, {nxt});")
+            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {off}, {bx.np2}, {bx.nl2}, "
+                         f"{bx.kp}, {bx.kl1}, {bx.kl2}>(T, S, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
