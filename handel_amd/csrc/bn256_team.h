@@ -85,7 +85,10 @@ HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
   for (int i = 0; i < kRedcSteps; i++) {
     uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
 #pragma unroll
-    for (int j = 0; j < 10; j++) a.c[i + j] += (uint64_t)q * p_limb(j);
+    for (int j = 0; j < 10; j++) {
+      a.c[i + j] += (uint64_t)q * p_limb(j);
+      asm("" : "+v"(a.c[i + j]));  // no reassociation into per-column chains
+    }
     a.c[i + 1] += a.c[i] >> 26;
   }
   uint32_t x[10];

@@ -130,23 +130,67 @@ HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t 
 
 // One job: sum of NP products of LDS operands plus NL R-shifted linear terms,
 // reduced once. Entries from `base`: NP x (u, v), NL x term, dst.
+//
+// Issue order matters more than instruction count here: with one wave per
+// SIMD nothing hides the latency of a dependent v_mad_u64_u32, and left alone
+// the scheduler hoists every operand load of the job to the top (24 x 10
+// VGPRs for a 12-product job) and, out of registers, walks the product column
+// by column through ONE accumulator — a serial chain of dependent mads. Each
+// product therefore runs in its own scheduling region (operand-scanning order:
+// the 100 mads of a product hit 19 different columns, so consecutive mads are
+// independent), with the next product's operands loaded at the top of the
+// region so the LDS latency overlaps the current product's mads.
+// acc += x * y in operand-scanning order, each partial product ONE
+// v_mad_u64_u32 into its column. The empty asm after each mad keeps LLVM from
+// reassociating a column's terms into a fresh serial chain (sum the products
+// of column k in a temporary, then add it to the accumulator), which is what
+// it does otherwise; the columns then stay independent chains of NP mads.
+HG_DEV void acc_mad_pinned(Acc& a, const Fp& x, const Fp& y) {
+#pragma unroll
+  for (int i = 0; i < 10; i++)
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      a.c[i + j] += (uint64_t)x.l[i] * y.l[j];
+      asm("" : "+v"(a.c[i + j]));
+    }
+}
+template <int W, int NP>
+HG_DEV void x_products(const Team& T, const uint32_t (&w)[W], int base, Acc& acc) {
+  if constexpr (NP > 0) {
+    Fp a, b;
+    ld_fp(a, x_at(T, x_off(w, base)));
+    ld_fp(b, x_at(T, x_off(w, base + 1)));
+    x_for<NP>([&](auto p) {
+      Fp a2, b2;
+      if constexpr (p + 1 < NP) {
+        ld_fp(a2, x_at(T, x_off(w, base + 2 * (p + 1))));
+        ld_fp(b2, x_at(T, x_off(w, base + 2 * (p + 1) + 1)));
+      }
+      acc_mad_pinned(acc, a, b);
+      // pin the columns here: the mads of product p stay in this region
+      // (and are not sunk past the store's branch with the rest of the job)
+#pragma unroll
+      for (int c = 0; c < 21; c++) asm volatile("" : "+v"(acc.c[c]));
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (p + 1 < NP) {
+        a = a2;
+        b = b2;
+      }
+    });
+  }
+}
 template <int W, int NP, int NL, int KL>
 HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst) {
   Acc acc;
   acc_zero(acc);
-  x_for<NP>([&](auto p) {
-    Fp a, b;
-    ld_fp(a, x_at(T, x_off(w, base + 2 * p)));
-    ld_fp(b, x_at(T, x_off(w, base + 2 * p + 1)));
-    acc_mad(acc, a, b);
-  });
   constexpr int lbase = 2 * NP;
   if constexpr (NL > 0) {
     uint32_t val[10];
     x_lincomb<W, NL, KL>(T, w, base + lbase, val);
 #pragma unroll
-    for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] += val[l];
+    for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] = val[l];
   }
+  x_products<W, NP>(T, w, base, acc);
   dst = x_off(w, base + lbase + NL);
   if constexpr (NL > 0) acc_reduce_wide(r, acc);  // linear terms: result < 31p
   else acc_reduce(r, acc);                        // products only: < 2p, one subtraction
