@@ -127,7 +127,13 @@ def pmc_traffic():
     import csv
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.csv")), key=os.path.getmtime)
+    import re
+
+    # newest = highest round/version in the name (mtimes are not kept by git or the box snapshot)
+    def key(path):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.csv")), key=key)
     for path in reversed(files):
         vals = {}
         with open(path) as f:
