@@ -11,7 +11,6 @@ function of (msg, range, bitset, sig), so batching cannot change them.
 
 from __future__ import annotations
 
-from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -19,15 +18,7 @@ import numpy as np
 from . import partitioner as part
 from ._lib import HG_ERR_SIG_UNMARSHAL, HG_OK
 from .engine import REQ_DTYPE, Engine
-
-
-@dataclass
-class IncomingSig:
-    """processing.go:61-66 incomingSig: origin, level, multisig."""
-    origin: int
-    level: int
-    bits: Sequence[bool]
-    sig: bytes
+from .sigprocessing import IncomingSig, MultiSig, bits_to_int, int_to_words
 
 
 class BatchVerifier:
@@ -46,8 +37,11 @@ class BatchVerifier:
         nw = 0
         sigs = bytearray()
         for i, (lo, size, bits, sig) in enumerate(items):
-            w = part.bits_to_words(bits)
-            reqs[i] = (lo, len(bits), size, nw)
+            if isinstance(bits, MultiSig):
+                w, bitlen = int_to_words(bits.bits, bits.bitlen), bits.bitlen
+            else:
+                w, bitlen = part.bits_to_words(bits), len(bits)
+            reqs[i] = (lo, bitlen, size, nw)
             words.append(w)
             nw += len(w)
             s = bytes(sig)
@@ -58,11 +52,17 @@ class BatchVerifier:
     def verify_levels(self, sigs: Sequence[IncomingSig]) -> List[Optional[str]]:
         """verifySignature (processing.go:342-368) for each incoming sig, as
         seen by node `node_id`; returns None or the reference's error text."""
+        return self.verify_nodes([(self.node_id, s) for s in sigs])
+
+    def verify_nodes(self, items_in: Sequence[Tuple[int, IncomingSig]]) -> List[Optional[str]]:
+        """verify_levels for signatures addressed to different nodes of the
+        same registry (several Handel instances in one process share a GPU
+        context: sigprocessing.SharedBatcher)."""
         items, errs = [], []
-        for s in sigs:
+        for node_id, s in items_in:
             try:
-                lo, hi = part.range_level(self.node_id, self.n, s.level)
-                items.append((lo, hi - lo, s.bits, s.sig))
+                lo, hi = part.range_level(node_id, self.n, s.level)
+                items.append((lo, hi - lo, s.ms, s.ms.sig))
                 errs.append(None)
             except part.PartitionerError as e:
                 items.append((0, 0, [], bytes(64)))
@@ -95,7 +95,7 @@ class BatchVerifier:
             if len(sig) != 64:  # x/crypto G1.Unmarshal wants exactly 64 bytes
                 out[i] = self.eng.code_string(HG_ERR_SIG_UNMARSHAL)
                 continue
-            todo.append(IncomingSig(0, level, bits, sig))
+            todo.append(IncomingSig(0, level, MultiSig(len(bits), bits_to_int(bits), sig)))
             where.append(i)
         for i, e in zip(where, self.verify_levels(todo) if todo else []):
             out[i] = e

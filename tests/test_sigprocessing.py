@@ -1,0 +1,319 @@
+"""Batched signature processing (handel_amd/sigprocessing.py) on CPU with fake
+verifiers: the reference's own processing/store tests restated
+(processing_test.go:17-50, store_test.go:69-195), the K-slot selection against
+a transliteration of readTodos (processing.go:171-220), and the shared
+multi-instance batcher."""
+
+import random
+import threading
+
+import pytest
+
+from handel_amd import sigprocessing as S
+
+
+def full_ms(level):
+    """util_test.go:116-141 fullBitset/fullSig: 2^(level-1) set bits (1 at level 0)."""
+    size = 1 << (level - 1 if level else 0)
+    return S.MultiSig(size, (1 << size) - 1, b"fake")
+
+
+def full_incoming(level):
+    return S.IncomingSig(origin=0, level=level, ms=full_ms(level))
+
+
+class EvaluatorLevel:
+    """processing_test.go:10-15."""
+
+    def evaluate(self, sp):
+        return sp.level
+
+
+def test_sig_processing_strategy():
+    """processing_test.go:17-50 TestSigProcessingStrategy (batch = 1)."""
+    sig0, sig1, sig2 = full_incoming(0), full_incoming(1), full_incoming(2)
+    ss = S.BatchedEvaluatorProcessing(lambda sigs: [None] * len(sigs), EvaluatorLevel(), batch=1)
+    assert len(ss.todos) == 0
+    ss.add(sig2)
+    assert len(ss.todos) == 1
+    assert ss.process_step() is False
+    assert len(ss.todos) == 0
+    # level-0 signatures are discarded, higher levels verified first
+    for s in (sig0, sig1, sig2, sig0):
+        ss.add(s)
+    ss.process_step()
+    assert len(ss.todos) == 1 and ss.todos[0] is sig1
+    ss.add(S.DEATH_PILL)
+    assert ss.process_step() is True
+    published = [ss.out.get_nowait() for _ in range(ss.out.qsize())]
+    assert published == [sig2, sig2, S.CLOSED]
+
+
+def reference_read_todos(todos, evaluate):
+    """processing.go:183-220 verbatim: (best, newTodos)."""
+    new, best, best_mark = [], None, 0
+    for pair in todos:
+        if pair.ms is None:
+            continue
+        mark = evaluate(pair)
+        if mark > 0:
+            if mark <= best_mark:
+                new.append(pair)
+            else:
+                if best is not None:
+                    new.append(best)
+                best, best_mark = pair, mark
+    return best, new
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_k1_matches_reference_loop(seed):
+    rng = random.Random(seed)
+    todos = [S.IncomingSig(origin=i, level=rng.randrange(1, 12), ms=None if rng.random() < 0.1 else full_ms(1))
+             for i in range(rng.randrange(1, 40))]
+    marks = {id(t): rng.choice([0, 0, 1, 2, 3, 5, 8]) for t in todos}
+
+    class Ev:
+        def evaluate(self, sp):
+            return marks[id(sp)]
+
+    want_best, want_new = reference_read_todos(todos, Ev().evaluate)
+    p = S.BatchedEvaluatorProcessing(lambda s: [None] * len(s), Ev(), batch=1)
+    p.todos = list(todos)
+    done, got = p.read_todos()
+    assert not done
+    assert got == ([want_best] if want_best is not None else [])
+    assert p.todos == want_new
+
+
+@pytest.mark.parametrize("k", [2, 5, 64])
+def test_k_slots_pick_the_k_best(k):
+    rng = random.Random(k)
+    todos = [S.IncomingSig(origin=i, level=1, ms=full_ms(1)) for i in range(50)]
+    marks = {id(t): rng.randrange(0, 10) for t in todos}
+    p = S.BatchedEvaluatorProcessing(lambda s: [None] * len(s), type("E", (), {"evaluate": lambda self, sp: marks[id(sp)]})(),
+                                     batch=k)
+    p.todos = list(todos)
+    _, best = p.read_todos()
+    positive = [t for t in todos if marks[id(t)] > 0]
+    # the K highest marks, stable (earliest first) among equal marks
+    want = sorted(positive, key=lambda t: -marks[id(t)])[:k]
+    assert best == want
+    assert sorted(map(id, p.todos)) == sorted(id(t) for t in positive if t not in want)
+    assert p.sig_checked_ct == len(want)
+    assert p.sig_suppressed == len(todos) - len(p.todos) - len(want)
+
+
+def test_individual_filter():
+    """processing.go:299-325: one individual signature per origin."""
+    f = S.IndividualSigFilter()
+    a = S.IncomingSig(origin=3, level=1, ms=full_ms(1), ind=True)
+    assert f.accept(a) and not f.accept(a)
+    assert f.accept(S.IncomingSig(origin=3, level=1, ms=full_ms(1)))  # multisigs always pass
+    assert f.accept(S.IncomingSig(origin=4, level=1, ms=full_ms(1), ind=True))
+
+
+def fake_combine(a, b):
+    return a  # util_test.go:97-99 fakeSig.Combine returns the receiver
+
+
+def test_store_replace_scores():
+    """store_test.go:136-195 TestStoreReplace (n = 8, node 1)."""
+    sigs = {lvl: S.IncomingSig(origin=0, level=lvl, ms=full_ms(lvl)) for lvl in range(4)}
+    cases = [
+        ([], [], [], 2, None),
+        ([2, 2], [999980, 0], [True, False], 2, sigs[2].ms),
+        ([0, 1, 2, 3], [1000000, 999990, 999980, 999970], [True, True, True, True], 2, sigs[2].ms),
+    ]
+    for order, scores, rets, lvl, eq in cases:
+        st = S.Store(1, 8, fake_combine)
+        for li, score, ret in zip(order, scores, rets):
+            assert st.evaluate(sigs[li]) == score
+            assert (st.store(sigs[li]) is not None) == ret
+        ms, ok = st.best(lvl)
+        assert ms == eq and ok == (eq is not None)
+
+
+def test_store_unsafe_check_merge():
+    """store_test.go:69-134 TestStoreUnsafeCheckMerge (n = 8, node 0)."""
+    st = S.Store(0, 8, fake_combine)
+    p4 = S.IncomingSig(origin=1, level=3, ms=S.MultiSig(4, 0b0001, b"s"), ind=True, mapped_index=0)
+    s, b = st._unsafe_check_merge(p4)
+    assert b and s.bits & 1 and s.cardinality() == 1
+    st.store(p4)
+    s, b = st._unsafe_check_merge(p4)
+    assert not b and s is None
+    p46 = S.IncomingSig(origin=1, level=3, ms=S.MultiSig(4, 0b0101, b"s"))
+    s, b = st._unsafe_check_merge(p46)
+    assert b and s.bits == 0b0101
+    st.store(p46)
+    assert st.best(3)[0].bits == 0b0101
+    p67 = S.IncomingSig(origin=1, level=3, ms=S.MultiSig(4, 0b1100, b"s"))
+    s, b = st._unsafe_check_merge(p67)
+    assert b and s.bits == 0b1101 and s.cardinality() == 3
+
+
+def test_store_merge_combines_signatures():
+    """Disjoint bitsets merge and the signatures are combined (store.go:196-201),
+    then verified individual signatures complete the set (store.go:215-223)."""
+    calls = []
+
+    def comb(a, b):
+        calls.append((a, b))
+        return b"(" + a + b"+" + b + b")"
+
+    st = S.Store(0, 8, comb)
+    st.store(S.IncomingSig(origin=4, level=3, ms=S.MultiSig(4, 0b0001, b"i0"), ind=True, mapped_index=0))
+    st.store(S.IncomingSig(origin=5, level=3, ms=S.MultiSig(4, 0b0110, b"m12")))
+    best = st.best(3)[0]
+    assert best.bits == 0b0111
+    assert best.sig == b"(i0+m12)"
+    assert st.evaluate(S.IncomingSig(origin=6, level=3, ms=S.MultiSig(4, 0b1000, b"m3"))) == 1000000 - 30
+
+
+def test_processing_loop_publishes_valid_in_batches():
+    seen_batches = []
+
+    def verify(sigs):
+        seen_batches.append(len(sigs))
+        return [None if s.origin % 3 else "handel: bn256: signature invalid" for s in sigs]
+
+    logs = []
+    p = S.BatchedEvaluatorProcessing(verify, S.Evaluator1(), batch=8, log=lambda k, v: logs.append((k, v)))
+    sigs = [S.IncomingSig(origin=i, level=1, ms=full_ms(1)) for i in range(1, 41)]
+    for s in sigs:
+        p.add(s)
+    p.start()
+    got = []
+    while len(got) < sum(1 for s in sigs if s.origin % 3):
+        got.append(p.verified().get(timeout=10))
+    p.stop()
+    assert p.verified().get(timeout=10) is S.CLOSED
+    assert {s.origin for s in got} == {s.origin for s in sigs if s.origin % 3}
+    assert all(b <= 8 for b in seen_batches) and sum(seen_batches) == 40
+    assert sum(1 for k, _ in logs if k == "verify") == sum(1 for s in sigs if s.origin % 3 == 0)
+    v = p.values()
+    assert v["sigCheckedCt"] == 40 and v["sigBatches"] == len(seen_batches)
+
+
+def test_shared_batcher_merges_instances():
+    calls = []
+    lock = threading.Lock()
+
+    def target(items):
+        with lock:
+            calls.append(len(items))
+        return [f"{node}:{s.origin}" for node, s in items]
+
+    b = S.SharedBatcher(target, max_batch=64, max_wait_us=20000)
+    results = {}
+
+    def inst(node):
+        sigs = [S.IncomingSig(origin=node * 100 + j, level=1, ms=full_ms(1)) for j in range(4)]
+        results[node] = b.bind(node)(sigs)
+
+    ts = [threading.Thread(target=inst, args=(n,)) for n in range(12)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    b.close()
+    for node, res in results.items():
+        assert res == [f"{node}:{node * 100 + j}" for j in range(4)]
+    assert sum(calls) == 48 and len(calls) < 12 and max(calls) <= 64
+
+
+def test_shared_batcher_surfaces_errors():
+    def target(items):
+        raise RuntimeError("hg_verify_aggregate failed")
+
+    b = S.SharedBatcher(target)
+    with pytest.raises(RuntimeError, match="hg_verify_aggregate"):
+        b.verify(0, [full_incoming(1)])
+    b.close()
+
+
+# ---------------------------------------------------------------------------
+# GPU: the golden 50-node registry and multisig packets through the batched
+# processing, the shared batcher and the store's GPU signature combine.
+
+
+def _golden_setup(engine):
+    import json
+    import os
+
+    from handel_amd import partitioner as part
+    from handel_amd import registry as REG
+    from handel_amd.processing import BatchVerifier
+
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(gold, "bn256_vectors.json")) as f:
+        ms = json.load(f)["multisig"]
+    recs = REG.read_records(os.path.join(gold, "registry_50.csv"))
+    bv = BatchVerifier(engine, REG.registry_bytes(recs), bytes.fromhex(ms["msg"]), node_id=ms["node"])
+    reqs = [r for r in ms["requests"] if r["level"] is not None]
+    sigs = []
+    for i, r in enumerate(reqs):
+        bits, sig = part.multisig_unmarshal(bytes.fromhex(r["multisig"]))
+        sigs.append(S.IncomingSig(origin=i, level=r["level"], ms=S.MultiSig(len(bits), S.bits_to_int(bits), sig)))
+    return bv, ms["node"], reqs, sigs
+
+
+@pytest.mark.gpu
+def test_gpu_batched_processing_golden(engine):
+    bv, _, reqs, sigs = _golden_setup(engine)
+    logs = []
+    p = S.BatchedEvaluatorProcessing(bv.verify_levels, S.Evaluator1(), batch=16, log=lambda k, v: logs.append(v))
+    for s in sigs:
+        p.add(s)
+    while p.todos:
+        p.process_step()
+    published = [p.out.get_nowait() for _ in range(p.out.qsize())]
+    want_ok = {s.origin for s, r in zip(sigs, reqs) if r["code"] == 0}
+    assert {s.origin for s in published} == want_ok
+    assert len(logs) == len(sigs) - len(want_ok)
+    assert all(isinstance(e, str) and e.startswith("handel: ") for e in logs)
+    assert p.batches == (len(sigs) + 15) // 16
+
+
+@pytest.mark.gpu
+def test_gpu_shared_batcher_golden(engine):
+    bv, node, reqs, sigs = _golden_setup(engine)
+    b = S.SharedBatcher(bv.verify_nodes, max_batch=4096, max_wait_us=50000)
+    out = {}
+
+    def inst(k):
+        mine = sigs[k::4]
+        out[k] = list(zip(mine, b.bind(node)(mine)))
+
+    ts = [threading.Thread(target=inst, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    b.close()
+    got = {s.origin: e for k in out for s, e in out[k]}
+    for s, r in zip(sigs, reqs):
+        assert (got[s.origin] is None) == (r["code"] == 0)
+    assert b.launches < 4
+
+
+@pytest.mark.gpu
+def test_gpu_store_combine_matches_oracle(engine):
+    from oracle import ref_lib as R
+
+    _, _, reqs, sigs = _golden_setup(engine)
+
+    def comb(a, b):
+        out, codes = engine.combine_g1(a, b)
+        assert codes[0] == 0
+        return out
+
+    ok = [s for s, r in zip(sigs, reqs) if r["code"] == 0]
+    a, b = ok[0].ms.sig, ok[1].ms.sig
+    assert comb(a, b) == R.g1_add(a, b)
+    st = S.Store(0, 8, comb)
+    st.store(S.IncomingSig(origin=1, level=3, ms=S.MultiSig(4, 0b0011, a)))
+    st.store(S.IncomingSig(origin=2, level=3, ms=S.MultiSig(4, 0b1100, b)))
+    best = st.best(3)[0]
+    assert best.bits == 0b1111 and best.sig == R.g1_add(a, b)
