@@ -44,12 +44,14 @@ void launch_verify(const CheckIn* in, int n, const LineCoef* tab, const PointG1*
 void launch_pair(const PointG1* g1s, const PointG2* g2s, int n, const LineCoef* tab, uint8_t* gt, hipStream_t s);
 // blocks/block_base: the aligned block sums of the registry (hg_registry_load);
 // level k block j at blocks[block_base[k] + j] for 1 <= k <= levels
-void launch_aggregate(const PointG2* reg, int nreg, const PointG2* blocks, const int* block_base, int levels,
+void launch_aggregate(const PointG2* wsum, int nreg, const PointG2* blocks, const int* block_base, int levels,
                       const AggRequest* reqs, int n, const uint64_t* words, int* order, void* partial_ws,
                       CheckIn* out, int32_t* codes, hipStream_t s);
 size_t agg_partial_bytes();  // workspace bytes per request for launch_aggregate
 size_t agg_fixed_bytes();    // plus this once
 void launch_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst, hipStream_t s);
+// byte-window subset sums: wsum[256 w + s] = sum of reg[8 w + j] over the bits j of s
+void launch_window_sums(const PointG2* reg, int nreg, PointG2* wsum, int nwin, hipStream_t s);
 void launch_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t* out, hipStream_t s);
 void launch_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, CheckIn* out, hipStream_t s);
 void launch_merge_codes(const int32_t* a, const int32_t* b, int n, int32_t* out, hipStream_t s);

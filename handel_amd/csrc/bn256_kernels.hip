@@ -270,11 +270,42 @@ __global__ __launch_bounds__(64) void k_block_sums(const PointG2* src, int nsrc,
   dst[j] = o;
 }
 
-static constexpr int kAggPosCap = 4096;  // folded positions staged per pass (64 words)
+// Byte-window subset sums (hg_registry_load): for every aligned 8-key window w
+// of the registry and every subset s of its keys, wsum[256 w + s] = the sum of
+// reg[8 w + j] over the bits j of s (slots past the registry are absent). The
+// fold then adds ONE table point per nonzero byte of the bitset instead of one
+// key per set bit: 256 points x 176 B per 8 keys (22.5 MB for N = 4000) of HBM
+// traded for ~2.5x fewer additions on the aggregation's critical path.
+__global__ __launch_bounds__(64) void k_window_sums(const PointG2* reg, int nreg, PointG2* wsum, int nwin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nwin * 256) return;
+  const int w = i >> 8, sub = i & 255;
+  G2J acc;
+  g2_set_inf(acc);
+  for (int j = 0; j < 8; j++) {
+    const int slot = 8 * w + j;
+    if (!((sub >> j) & 1) || slot >= nreg || reg[slot].inf) continue;
+    g2_madd(acc, acc, reg[slot].x, reg[slot].y);
+  }
+  PointG2 o;
+  o.pad[0] = o.pad[1] = o.pad[2] = 0;
+  if (g2_is_inf(acc)) {
+    f2_zero(o.x);
+    f2_zero(o.y);
+    o.inf = 1;
+  } else {
+    g2_affine(o.x, o.y, acc);
+    o.inf = 0;
+  }
+  wsum[i] = o;
+}
+
+static constexpr int kAggPosCap = 64 * 8;  // window entries staged per pass (one word per lane)
 
 // The per-request plan shared by the ordering and the fold kernels: set count,
-// whether the block complement applies (and at which level), keys to fold m,
-// and the lanes L that fold them.
+// whether the block complement applies (and at which level), table points to
+// fold m (nonzero bytes of the folded mask in registry-aligned windows), and
+// the lanes L that fold them.
 struct AggPlan {
   uint32_t cnt, m;
   int k, lanes;
@@ -286,7 +317,31 @@ HG_DEV uint64_t agg_word(const AggRequest& q, const uint64_t* words, uint32_t wi
   if (lo + 64 > q.bitlen) w &= (1ull << (q.bitlen - lo)) - 1;
   return w;
 }
-HG_DEV AggPlan agg_plan(const AggRequest& q, uint32_t cnt, int nreg, int levels) {
+// request word wi of the folded mask (complemented within bitlen when comp); 0 outside
+HG_DEV uint64_t agg_mask_word(const AggRequest& q, const uint64_t* words, int wi, bool comp) {
+  const int nw = (int)((q.bitlen + 63) / 64);
+  if (wi < 0 || wi >= nw) return 0;
+  uint64_t w = words[q.word_offset + wi];
+  if (comp) w = ~w;
+  const uint32_t lo = (uint32_t)wi * 64;
+  if (lo + 64 > q.bitlen) w &= (1ull << (q.bitlen - lo)) - 1;
+  return w;
+}
+// registry-aligned word v of the mask: bit j = registry slot (offset & ~7) + 64 v + j
+HG_DEV uint64_t agg_rword(const AggRequest& q, const uint64_t* words, int v, bool comp) {
+  const int sh = (int)(q.offset & 7u);
+  const uint64_t hi = agg_mask_word(q, words, v, comp);
+  if (sh == 0) return hi;
+  return (hi << sh) | (agg_mask_word(q, words, v - 1, comp) >> (64 - sh));
+}
+HG_DEV uint32_t agg_nrwords(const AggRequest& q) { return (q.bitlen + (q.offset & 7u) + 63) / 64; }
+HG_DEV uint32_t nz_bytes(uint64_t x) {
+  x |= x >> 4;
+  x |= x >> 2;
+  x |= x >> 1;
+  return __popcll(x & 0x0101010101010101ull);
+}
+HG_DEV AggPlan agg_plan(const AggRequest& q, uint32_t cnt, uint32_t nz_set, uint32_t nz_unset, int nreg, int levels) {
   AggPlan p;
   p.cnt = cnt;
   const uint32_t bitlen = q.bitlen;
@@ -295,8 +350,8 @@ HG_DEV AggPlan agg_plan(const AggRequest& q, uint32_t cnt, int nreg, int levels)
   const bool aligned = bitlen > 0 && k <= levels && (q.offset & ((1u << k) - 1)) == 0 &&
                        (bitlen == (1u << k) || q.offset + bitlen == (uint32_t)nreg);
   p.k = k;
-  p.comp = aligned && k > 0 && 2 * cnt > bitlen;
-  p.m = p.comp ? bitlen - cnt : cnt;
+  p.comp = aligned && k > 0 && nz_unset < nz_set;
+  p.m = p.comp ? nz_unset : nz_set;
   int L = 1;
   while (L < 64 && 2u * (uint32_t)(2 * L) <= p.m + 1) L *= 2;  // L ~ m / 2, power of two
   p.lanes = L;
@@ -313,43 +368,52 @@ struct AggSched {
   int req_start[8];   // first entry of class c in order[]
   int nreq[7];
 };
-__global__ __launch_bounds__(1024) void k_agg_order(const AggRequest* reqs, int n, const uint64_t* words,
-                                                    const int32_t* codes, int nreg, int levels, int* order,
-                                                    AggPlan* plans, AggSched* sched) {
-  constexpr int kSub = 64;  // cost sub-buckets inside a lane class
-  __shared__ int hist[7 * kSub];
-  __shared__ int start[7 * kSub];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 7 * kSub; i += blockDim.x) hist[i] = 0;
-  __syncthreads();
-  auto key = [&](int r, bool store) -> int {
-    AggPlan p;
-    if (codes[r] != HG_OK) {
-      p.cnt = 0;
-      p.m = 0;
-      p.k = 0;
-      p.lanes = 1;
-      p.comp = false;
-    } else {
-      const AggRequest q = reqs[r];
-      uint32_t cnt = 0;
-      for (uint32_t wi = 0; wi < (q.bitlen + 63) / 64; wi++) cnt += __popcll(agg_word(q, words, wi));
-      p = agg_plan(q, cnt, nreg, levels);
+// Plan of every request (one thread each, grid-wide): counts, complement
+// decision, lanes; and its sort key for k_agg_order.
+static constexpr int kAggSub = 64;  // cost sub-buckets inside a lane class
+__global__ __launch_bounds__(64) void k_agg_plan(const AggRequest* reqs, int n, const uint64_t* words,
+                                                 const int32_t* codes, int nreg, int levels, AggPlan* plans,
+                                                 int* keys) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  AggPlan p;
+  if (codes[r] != HG_OK) {
+    p.cnt = 0;
+    p.m = 0;
+    p.k = 0;
+    p.lanes = 1;
+    p.comp = false;
+  } else {
+    const AggRequest q = reqs[r];
+    uint32_t cnt = 0, nzs = 0, nzu = 0;
+    for (uint32_t wi = 0; wi < (q.bitlen + 63) / 64; wi++) cnt += __popcll(agg_word(q, words, wi));
+    for (uint32_t v = 0; v < agg_nrwords(q); v++) {
+      nzs += nz_bytes(agg_rword(q, words, (int)v, false));
+      nzu += nz_bytes(agg_rword(q, words, (int)v, true));
     }
-    if (store) plans[r] = p;
-    int lg = 0;
-    while ((1 << lg) < p.lanes) lg++;
-    const uint32_t per = (p.m + p.lanes - 1) / p.lanes;  // keys per lane
-    return (6 - lg) * kSub + (kSub - 1 - (int)(per < (uint32_t)(kSub - 1) ? per : kSub - 1));
-  };
-  for (int r = tid; r < n; r += blockDim.x) atomicAdd(&hist[key(r, true)], 1);
+    p = agg_plan(q, cnt, nzs, nzu, nreg, levels);
+  }
+  plans[r] = p;
+  int lg = 0;
+  while ((1 << lg) < p.lanes) lg++;
+  const uint32_t per = (p.m + p.lanes - 1) / p.lanes;  // table points per lane
+  keys[r] = (6 - lg) * kAggSub + (kAggSub - 1 - (int)(per < (uint32_t)(kAggSub - 1) ? per : kAggSub - 1));
+}
+
+__global__ __launch_bounds__(1024) void k_agg_order(int n, const int* keys, int* order, AggSched* sched) {
+  __shared__ int hist[7 * kAggSub];
+  __shared__ int start[7 * kAggSub];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 7 * kAggSub; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  for (int r = tid; r < n; r += blockDim.x) atomicAdd(&hist[keys[r]], 1);
   __syncthreads();
   if (tid == 0) {
     int acc = 0, tasks = 0;
     for (int c = 0; c < 7; c++) {
       int nc = 0;
       sched->req_start[c] = acc;
-      for (int b = c * kSub; b < (c + 1) * kSub; b++) {
+      for (int b = c * kAggSub; b < (c + 1) * kAggSub; b++) {
         start[b] = acc;
         acc += hist[b];
         nc += hist[b];
@@ -363,18 +427,19 @@ __global__ __launch_bounds__(1024) void k_agg_order(const AggRequest* reqs, int 
     sched->task_start[7] = tasks;
   }
   __syncthreads();
-  for (int r = tid; r < n; r += blockDim.x) order[atomicAdd(&start[key(r, false)], 1)] = r;
+  for (int r = tid; r < n; r += blockDim.x) order[atomicAdd(&start[keys[r]], 1)] = r;
 }
 
 // One wave per task: 64 / L requests of the same lane count L, one group of L
-// lanes each. Per group: compaction of the keys to fold (L words per pass,
-// segmented prefix sums), ceil(m / L) mixed additions per lane, then a
-// log2(L)-level LDS tree; the group root is the request's partial sum.
-__global__ __launch_bounds__(64) void k_aggregate(const PointG2* reg, const AggRequest* reqs,
+// lanes each. Per group: compaction of the nonzero window bytes of the folded
+// mask (one registry-aligned word = 8 windows per lane and pass, segmented
+// prefix sums), ceil(m / L) mixed additions of window subset sums per lane,
+// then a log2(L)-level LDS tree; the group root is the request's partial sum.
+__global__ __launch_bounds__(64) void k_aggregate(const PointG2* wsum, const AggRequest* reqs,
                                                   const uint64_t* words, const int* order, const AggPlan* plans,
                                                   const AggSched* sched, AggPartial* partial) {
   __shared__ G2J part[64];
-  __shared__ uint16_t pos[kAggPosCap];
+  __shared__ uint32_t pos[kAggPosCap];
   __shared__ uint32_t cnt_lds[64];
   __shared__ uint32_t nw_lds[64];
   const int t = blockIdx.x;
@@ -399,43 +464,37 @@ __global__ __launch_bounds__(64) void k_aggregate(const PointG2* reg, const AggR
     pl = plans[r];
   }
   const bool active = has && pl.cnt > 0;  // level errors and empty bitsets fold nothing
-  const uint32_t nwords = active ? (q.bitlen + 63) / 64 : 0;
-  nw_lds[lane] = nwords;
+  const uint32_t nrw = active ? agg_nrwords(q) : 0;
+  const uint32_t win0 = q.offset >> 3;  // first window of the request
+  nw_lds[lane] = nrw;
   __syncthreads();
   uint32_t maxw = 0;
   for (int i = 0; i < 64; i += L) maxw = nw_lds[i] > maxw ? nw_lds[i] : maxw;  // wave-uniform
   G2J acc;
   g2_set_inf(acc);
-  for (uint32_t w0 = 0; w0 < maxw; w0 += L) {
-    const uint32_t wi = w0 + l;
-    uint64_t mb = 0;
-    if (wi < nwords) {
-      mb = agg_word(q, words, wi);
-      if (pl.comp) {
-        mb = ~mb;
-        const uint32_t lo = wi * 64;
-        if (lo + 64 > q.bitlen) mb &= (1ull << (q.bitlen - lo)) - 1;
-      }
-    }
-    const uint32_t pc = __popcll(mb);
+  for (uint32_t v0 = 0; v0 < maxw; v0 += L) {
+    const uint32_t v = v0 + l;
+    const uint64_t mb = v < nrw ? agg_rword(q, words, (int)v, pl.comp) : 0;
+    const uint32_t pc = nz_bytes(mb);
     cnt_lds[lane] = pc;
     __syncthreads();
     for (int d = 1; d < L; d <<= 1) {  // inclusive prefix inside the group
-      const uint32_t v = l >= d ? cnt_lds[lane - d] : 0;
+      const uint32_t x = l >= d ? cnt_lds[lane - d] : 0;
       __syncthreads();
-      cnt_lds[lane] += v;
+      cnt_lds[lane] += x;
       __syncthreads();
     }
     const uint32_t total = cnt_lds[gbase + L - 1];
-    uint32_t at = gbase * 64 + cnt_lds[lane] - pc;  // group region: 64 entries per lane
-    while (mb) {
-      const int b = __builtin_ctzll(mb);
-      pos[at++] = (uint16_t)(l * 64 + b);
-      mb &= mb - 1;
+    uint32_t at = gbase * 8 + cnt_lds[lane] - pc;  // group region: 8 entries per lane
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t byte = (uint32_t)(mb >> (8 * j)) & 255u;
+      if (byte) pos[at++] = ((uint32_t)(l * 8 + j) << 8) | byte;
     }
     __syncthreads();
     for (uint32_t e = l; e < total; e += L) {
-      const PointG2& P = reg[q.offset + w0 * 64 + pos[gbase * 64 + e]];
+      const uint32_t ent = pos[gbase * 8 + e];
+      const PointG2& P = wsum[(size_t)(win0 + v0 * 8 + (ent >> 8)) * 256 + (ent & 255u)];
       if (!P.inf) g2_madd(acc, acc, P.x, P.y);
     }
     __syncthreads();
@@ -595,7 +654,7 @@ void launch_g1_mul(const PointG1* base, const uint8_t* scalars, int n, PointG1* 
 }
 void launch_hash_point(const uint32_t* k, PointG1* out, hipStream_t s) { k_hash_point<<<1, 64, 0, s>>>(k, out); }
 void launch_g2_lines(LineCoef* tab, hipStream_t s) { k_g2_lines<<<1, 64, 0, s>>>(tab); }
-void launch_aggregate(const PointG2* reg, int nreg, const PointG2* blocks, const int* block_base, int levels,
+void launch_aggregate(const PointG2* wsum, int nreg, const PointG2* blocks, const int* block_base, int levels,
                       const AggRequest* reqs, int n, const uint64_t* words, int* order, void* partial_ws,
                       CheckIn* out, int32_t* codes, hipStream_t s) {
   AggPartial* partial = (AggPartial*)partial_ws;
@@ -604,13 +663,18 @@ void launch_aggregate(const PointG2* reg, int nreg, const PointG2* blocks, const
   for (int k = 0; k < 24; k++) bi.base[k] = k <= bi.levels ? block_base[k] : 0;
   if (n <= 0) return;
   AggPlan* plans = (AggPlan*)((uint8_t*)partial_ws + (size_t)n * sizeof(AggPartial));
-  AggSched* sched = (AggSched*)(plans + n);
-  k_agg_order<<<1, 1024, 0, s>>>(reqs, n, words, codes, nreg, bi.levels, order, plans, sched);
-  k_aggregate<<<n, 64, 0, s>>>(reg, reqs, words, order, plans, sched, partial);
+  int* keys = (int*)(plans + n);
+  AggSched* sched = (AggSched*)(keys + n);
+  k_agg_plan<<<nblk(n, 64), 64, 0, s>>>(reqs, n, words, codes, nreg, bi.levels, plans, keys);
+  k_agg_order<<<1, 1024, 0, s>>>(n, keys, order, sched);
+  k_aggregate<<<n, 64, 0, s>>>(wsum, reqs, words, order, plans, sched, partial);
   k_agg_finish<<<nblk(n, 64), 64, 0, s>>>(blocks, bi, reqs, n, partial, out, codes);
 }
-size_t agg_partial_bytes() { return sizeof(AggPartial) + sizeof(AggPlan); }
+size_t agg_partial_bytes() { return sizeof(AggPartial) + sizeof(AggPlan) + sizeof(int); }
 size_t agg_fixed_bytes() { return sizeof(AggSched); }
+void launch_window_sums(const PointG2* reg, int nreg, PointG2* wsum, int nwin, hipStream_t s) {
+  if (nwin > 0) k_window_sums<<<nblk(nwin * 256, 64), 64, 0, s>>>(reg, nreg, wsum, nwin);
+}
 void launch_block_sums(const PointG2* src, int nsrc, PointG2* dst, int ndst, hipStream_t s) {
   if (ndst > 0) k_block_sums<<<nblk(ndst, 64), 64, 0, s>>>(src, nsrc, dst, ndst);
 }

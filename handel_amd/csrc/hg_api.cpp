@@ -158,6 +158,8 @@ struct hg_ctx {
   size_t nreg = 0;
   // aligned block sums of the registry (level k block j at blocks[block_base[k] + j])
   DevBuf<PointG2> blocks;
+  // subset sums of every aligned 8-key window (256 per window), the fold's table
+  DevBuf<PointG2> wsum;
   std::vector<int> block_base = std::vector<int>(24, 0);
   int block_levels = 0;
   // workspaces
@@ -348,6 +350,14 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
     if (rc) return rc;
     HG_CHECK(c, hipStreamSynchronize(c->stream));
   }
+  const size_t nwin = (n + 7) / 8;
+  if (nwin) {
+    HG_CHECK(c, c->wsum.ensure(nwin * 256));
+    launch_window_sums(c->reg.p, (int)n, c->wsum.p, (int)nwin, c->stream);
+    rc = check_launch(c);
+    if (rc) return rc;
+    HG_CHECK(c, hipStreamSynchronize(c->stream));
+  }
   c->block_levels = K;
   return HG_OK;
 }
@@ -421,7 +431,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   HG_CHECK(c, c->checks.ensure(n));
   HG_CHECK(c, c->order.ensure(n));
   HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
-  launch_aggregate(c->reg.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
+  launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
                    d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
   if (d_agg) {
     HG_CHECK(c, c->pts2.ensure(n));

@@ -234,3 +234,35 @@ def test_aggregate_block_complement_matches_oracle(engine):
     assert list(codes) == list(want)
     for i in range(len(reqs)):
         assert agg[128 * i:128 * (i + 1)] == want_agg[128 * i:128 * (i + 1)], f"agg {i} {ranges[i]}"
+
+
+def test_aggregate_unaligned_ranges_match_oracle(engine):
+    """Ranges that are not Handel level blocks (offsets off the 8-key window
+    grid, lengths that straddle windows and words): the window subset-sum fold
+    must shift the bitset into registry-aligned windows and never take the
+    block complement."""
+    n_reg = 200
+    ks = F.scalars(n_reg, seed=b"agg-unaligned")
+    reg = R.g2_scalar_base(F.scalar_bytes(ks))
+    assert list(engine.registry_load(reg)) == [0] * n_reg
+    msg = F.LIB_MESSAGE
+    assert engine.set_message(msg) == 0
+    ranges = [(3, 70), (13, 5), (101, 99), (7, 1), (63, 66), (1, 128), (129, 64), (0, 200), (190, 10)]
+    rng = np.random.default_rng(5)
+    bitsets = []
+    for i, (off, size) in enumerate(ranges):
+        p = [0.9, 0.5, 0.1][i % 3]
+        bits = [bool(b) for b in rng.random(size) < p]
+        if not any(bits):
+            bits[0] = True
+        bitsets.append(bits)
+    bitsets[2] = [True] * ranges[2][1]
+    reqs, words = F.pack_requests(ranges, bitsets)
+    sigs = O.g1_marshal(O.G1_GEN) * len(reqs)
+    codes, agg = engine.verify_aggregate(np.array(reqs, dtype=engine_req_dtype()), words, sigs, want_agg=True)
+    woff = np.array([r[3] for r in reqs], dtype=np.uint64)
+    want, want_agg = R.verify_aggregate(msg, reg, [r[0] for r in reqs], [r[1] for r in reqs],
+                                        [r[2] for r in reqs], words, woff, sigs, nthreads=4, want_agg=True)
+    assert list(codes) == list(want)
+    for i in range(len(reqs)):
+        assert agg[128 * i:128 * (i + 1)] == want_agg[128 * i:128 * (i + 1)], f"agg {i} {ranges[i]}"
