@@ -27,21 +27,6 @@
 #include "bn256_inv.h"
 
 #define HG_DEV __device__ __forceinline__
-#ifdef HG_EXP_TAIL
-// timing experiment only (wrong results): 1 = REDC q-loop + one parallel carry pass, 2 = no REDC
-#if HG_EXP_TAIL == 1
-#define EXP_BODY \
-  for (int i = 0; i < kRedcSteps; i++) { uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask; \
-    for (int j = 0; j < 10; j++) { a.c[i + j] += (uint64_t)q * p_limb(j); asm("" : "+v"(a.c[i + j])); } \
-    a.c[i + 1] += a.c[i] >> 26; } \
-  for (int j = 0; j < 10; j++) r.l[j] = ((uint32_t)a.c[kRedcSteps + j] & kMask) + (uint32_t)(a.c[kRedcSteps + j - 1] >> 26); \
-  return;
-#else
-#define EXP_BODY \
-  for (int j = 0; j < 10; j++) r.l[j] = ((uint32_t)a.c[kRedcSteps + j] & kMask) + (uint32_t)(a.c[kRedcSteps + j - 1] >> 26); \
-  return;
-#endif
-#endif
 
 namespace hg {
 
@@ -133,9 +118,6 @@ HG_DEV void acc_sqr(Acc& a, const Fp& x) {
 // (11 digits of 26 bits; the result T / R + q p / R < 2p before the final
 // conditional subtraction).
 HG_DEV void acc_reduce(Fp& r, Acc& a) {
-#ifdef HG_EXP_TAIL
-  EXP_BODY
-#endif
 #pragma unroll
   for (int i = 0; i < kRedcSteps; i++) {
     uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;

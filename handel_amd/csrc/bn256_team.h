@@ -81,9 +81,6 @@ HG_DEV void fp_reduce8(Fp& r, const uint32_t* x) {
 // (linear terms) + p, below 31p (generator-checked); a quotient estimate
 // (fp_reduce8) makes it canonical. Sums of products only use acc_reduce.
 HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
-#ifdef HG_EXP_TAIL
-  EXP_BODY
-#endif
 #pragma unroll
   for (int i = 0; i < kRedcSteps; i++) {
     uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
