@@ -1,5 +1,6 @@
 // bn256_inv.h — variable-time modular inversion mod p by Bernstein–Yang
-// divsteps ("safegcd", batches of 62 divsteps on 64-bit words), the
+// divsteps ("safegcd"; batches of 30 divsteps on 32-bit words on the device
+// path, the 62-divstep 64-bit form kept beside it), the
 // inversion behind fp_inv (final exponentiation's Fp6 norm inverse, affine
 // conversions).
 //
@@ -257,12 +258,194 @@ HG_HD void s62_to_words(uint32_t* w, const S62* r) {
   w[7] = (uint32_t)(a3 >> 32);
 }
 
-// plain integer inverse: w (8 LE words, value < p) <- w^-1 mod p
-HG_HD void inv_words(uint32_t* w) {
+// plain integer inverse on signed62 limbs (kept for comparison; the device
+// path uses the signed30 version below)
+HG_HD void inv_words62(uint32_t* w) {
   S62 x;
   words_to_s62(&x, w);
   modinv_var(&x);
   s62_to_words(w, &x);
+}
+
+// ---------------------------------------------------------------- signed30
+// The same algorithm on 32-bit words: batches of 30 divsteps on uint32, a
+// transition matrix of int32 entries, and 9-limb signed30 numbers updated with
+// int32 x int32 -> int64 multiply-adds (one v_mad_i64_i32 each). On gfx950 the
+// 64-bit version's 64x64 -> 128-bit products and 64-bit shifts cost several
+// 32-bit instructions each; here every divstep is 32-bit ALU work and every
+// matrix product is a native 32x32 -> 64 multiply-add.
+struct S30 {
+  int32_t v[9];
+};
+struct Mat30 {
+  int32_t u, v, q, r;
+};
+static constexpr uint32_t kM30 = 0x3fffffffu;
+#define HG_P30 0x1e089667, 0x2172b1b1, 0x0b5b59e1, 0x16e23448, 0x04dc21ee, 0x3fb2e186, 0x387f9aa6, 0x0078d2a8, 0x8fb5
+static constexpr uint32_t kPInv30 = 0x00e82557u;  // p^-1 mod 2^30 (tests check p * inv == 1)
+
+HG_HD int ctz32(uint32_t x) { return __builtin_ctz(x); }
+
+// 30 divsteps on the low words of f, g (eta = -delta); returns the new eta
+// and the transition matrix scaled by 2^30.
+HG_HD int32_t divsteps_30_var(int32_t eta, uint32_t f0, uint32_t g0, Mat30* t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t f = f0, g = g0, m, w;
+  int i = 30, limit, zeros;
+  for (;;) {
+    zeros = ctz32(g | (UINT32_MAX << i));
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {
+      uint32_t tmp;
+      eta = -eta;
+      tmp = f; f = g; g = 0u - tmp;
+      tmp = u; u = q; q = 0u - tmp;
+      tmp = v; v = r; r = 0u - tmp;
+      limit = (eta + 1) > i ? i : (eta + 1);
+      m = (UINT32_MAX >> (32 - limit)) & 63u;
+      w = (f * g * (f * f - 2)) & m;
+    } else {
+      limit = (eta + 1) > i ? i : (eta + 1);
+      m = (UINT32_MAX >> (32 - limit)) & 15u;
+      w = f + (((f + 1) & 4) << 1);
+      w = (0u - w * g) & m;
+    }
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t->u = (int32_t)u;
+  t->v = (int32_t)v;
+  t->q = (int32_t)q;
+  t->r = (int32_t)r;
+  return eta;
+}
+
+// [d, e] <- t [d, e] / 2^30 (mod p), keeping d, e in (-2p, p)
+HG_HD void update_de_30(S30* d, S30* e, const Mat30* t) {
+  const int32_t P[9] = {HG_P30};
+  const int32_t u = t->u, v = t->v, q = t->q, r = t->r;
+  const int32_t sd = d->v[8] >> 31, se = e->v[8] >> 31;
+  int32_t md = (u & sd) + (v & se);
+  int32_t me = (q & sd) + (r & se);
+  int64_t cd = (int64_t)u * d->v[0] + (int64_t)v * e->v[0];
+  int64_t ce = (int64_t)q * d->v[0] + (int64_t)r * e->v[0];
+  // choose md, me so that the low 30 bits of t [d, e] + p [md, me] vanish
+  md -= (int32_t)((kPInv30 * (uint32_t)cd + (uint32_t)md) & kM30);
+  me -= (int32_t)((kPInv30 * (uint32_t)ce + (uint32_t)me) & kM30);
+  cd += (int64_t)P[0] * md;
+  ce += (int64_t)P[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+  for (int i = 1; i < 9; i++) {
+    cd += (int64_t)u * d->v[i] + (int64_t)v * e->v[i] + (int64_t)P[i] * md;
+    ce += (int64_t)q * d->v[i] + (int64_t)r * e->v[i] + (int64_t)P[i] * me;
+    d->v[i - 1] = (int32_t)((uint32_t)cd & kM30);
+    cd >>= 30;
+    e->v[i - 1] = (int32_t)((uint32_t)ce & kM30);
+    ce >>= 30;
+  }
+  d->v[8] = (int32_t)cd;
+  e->v[8] = (int32_t)ce;
+}
+
+// [f, g] <- t [f, g] / 2^30 (exact), all 9 limbs
+HG_HD void update_fg_30(S30* f, S30* g, const Mat30* t) {
+  const int32_t u = t->u, v = t->v, q = t->q, r = t->r;
+  int64_t cf = (int64_t)u * f->v[0] + (int64_t)v * g->v[0];
+  int64_t cg = (int64_t)q * f->v[0] + (int64_t)r * g->v[0];
+  cf >>= 30;
+  cg >>= 30;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+  for (int i = 1; i < 9; i++) {
+    cf += (int64_t)u * f->v[i] + (int64_t)v * g->v[i];
+    cg += (int64_t)q * f->v[i] + (int64_t)r * g->v[i];
+    f->v[i - 1] = (int32_t)((uint32_t)cf & kM30);
+    cf >>= 30;
+    g->v[i - 1] = (int32_t)((uint32_t)cg & kM30);
+    cg >>= 30;
+  }
+  f->v[8] = (int32_t)cf;
+  g->v[8] = (int32_t)cg;
+}
+
+// r in (-2p, p) -> r * sign(sign) mod p in [0, p)
+HG_HD void normalize_30(S30* r, int32_t sign) {
+  const int32_t P[9] = {HG_P30};
+  int32_t x[9];
+  for (int i = 0; i < 9; i++) x[i] = r->v[i];
+  int32_t cond_add = x[8] >> 31;
+  for (int i = 0; i < 9; i++) x[i] += P[i] & cond_add;
+  const int32_t cond_negate = sign >> 31;
+  for (int i = 0; i < 9; i++) x[i] = (x[i] ^ cond_negate) - cond_negate;
+  for (int i = 0; i < 8; i++) {
+    x[i + 1] += x[i] >> 30;
+    x[i] &= (int32_t)kM30;
+  }
+  cond_add = x[8] >> 31;
+  for (int i = 0; i < 9; i++) x[i] += P[i] & cond_add;
+  for (int i = 0; i < 8; i++) {
+    x[i + 1] += x[i] >> 30;
+    x[i] &= (int32_t)kM30;
+  }
+  for (int i = 0; i < 9; i++) r->v[i] = x[i];
+}
+
+// x <- x^-1 mod p for 0 <= x < p (0 -> 0)
+HG_HD void modinv30_var(S30* x) {
+  S30 d = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
+  S30 e = {{1, 0, 0, 0, 0, 0, 0, 0, 0}};
+  S30 f = {{HG_P30}};
+  S30 g = *x;
+  int32_t eta = -1;  // eta = -delta, delta = 1
+  for (;;) {
+    Mat30 t;
+    eta = divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], &t);
+    update_de_30(&d, &e, &t);
+    update_fg_30(&f, &g, &t);
+    int32_t z = 0;
+    for (int i = 0; i < 9; i++) z |= g.v[i];
+    if (z == 0) break;
+  }
+  normalize_30(&d, f.v[8]);
+  *x = d;
+}
+
+// 8 LE 32-bit words <-> signed30 (bit 30 k + j of the value = bit j of limb k)
+HG_HD void words_to_s30(S30* r, const uint32_t* w) {
+  for (int k = 0; k < 9; k++) {
+    const int bit = 30 * k, wi = bit >> 5, sh = bit & 31;
+    uint64_t v = (uint64_t)w[wi] >> sh;
+    if (wi + 1 < 8) v |= (uint64_t)w[wi + 1] << (32 - sh);
+    r->v[k] = (int32_t)((uint32_t)v & kM30);
+  }
+}
+HG_HD void s30_to_words(uint32_t* w, const S30* r) {
+  for (int i = 0; i < 8; i++) w[i] = 0;
+  for (int k = 0; k < 9; k++) {
+    const int bit = 30 * k, wi = bit >> 5, sh = bit & 31;
+    const uint32_t v = (uint32_t)r->v[k];
+    w[wi] |= v << sh;
+    if (wi + 1 < 8 && sh > 2) w[wi + 1] |= v >> (32 - sh);
+  }
+}
+
+// plain integer inverse: w (8 LE words, value < p) <- w^-1 mod p
+HG_HD void inv_words(uint32_t* w) {
+  S30 x;
+  words_to_s30(&x, w);
+  modinv30_var(&x);
+  s30_to_words(w, &x);
 }
 
 }  // namespace inv

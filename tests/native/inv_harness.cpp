@@ -5,12 +5,14 @@
 
 #include "bn256_inv.h"
 
-int main() {
+int main(int argc, char** argv) {
+  const bool use62 = argc > 1;  // the signed62 form for comparison
   uint32_t w[8];
   for (;;) {
     for (int i = 0; i < 8; i++)
       if (scanf("%x", &w[i]) != 1) return 0;
-    hg::inv::inv_words(w);
+    if (use62) hg::inv::inv_words62(w);
+    else hg::inv::inv_words(w);
     for (int i = 0; i < 8; i++) printf("%08x ", w[i]);
     printf("\n");
   }
