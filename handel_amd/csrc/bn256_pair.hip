@@ -10,7 +10,7 @@ static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 // bn256.Pair(g1, g2).Marshal() for n pairs (GT = 1 when either is infinity)
 __global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* g2s, int n, const LineCoef* tab,
                                              uint8_t* gt_out) {
-  __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeamsPerBlock * kTeamWords];
   Team T = make_team(lds, kTeamWords);
   uint32_t* F = team_regs(T);
   int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(64) void k_pair(const PointG1* g1s, const PointG2* 
 //   op 0 a*b, 1 a^2 (merged products), 2 cyclotomic a^2, 3 a^p, 4 a^(p^2),
 //   5 a^-1, 6 conj(a), 7 a^u (cyclotomic), 8 final exponentiation
 __global__ __launch_bounds__(64) void k_fp12_op(int op, const uint8_t* a, const uint8_t* b, int n, uint8_t* out) {
-  __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeamsPerBlock * kTeamWords];
   Team T = make_team(lds, kTeamWords);
   uint32_t* F = T.base + kSlots * kFp12Words;
   int idx = blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);

@@ -40,6 +40,24 @@ HG_DEV void st_fp(uint32_t* p, const Fp& a) {
 #pragma unroll
   for (int i = 0; i < 10; i++) p[i] = a.l[i];
 }
+// 8-byte-aligned element access (every element of a team region: 40-byte
+// stride from an 8-aligned base): 64-bit LDS operations, so a 10-limb element
+// moves in 3 instructions (2 x ds_read2_b64 + ds_read_b64) instead of 5 x
+// ds_read2_b32 — at one wave per SIMD every issued instruction counts.
+HG_DEV void ld_fp_a8(Fp& r, const uint32_t* p) {
+  const uint64_t* q = (const uint64_t*)__builtin_assume_aligned(p, 8);
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint64_t v = q[i];
+    r.l[2 * i] = (uint32_t)v;
+    r.l[2 * i + 1] = (uint32_t)(v >> 32);
+  }
+}
+HG_DEV void st_fp_a8(uint32_t* p, const uint32_t* l) {
+  uint64_t* q = (uint64_t*)__builtin_assume_aligned(p, 8);
+#pragma unroll
+  for (int i = 0; i < 5; i++) q[i] = (uint64_t)l[2 * i] | ((uint64_t)l[2 * i + 1] << 32);
+}
 HG_DEV void ld_f2(Fp2& r, const uint32_t* f12, int k) {
   ld_fp(r.x, f12 + (2 * k) * 10);
   ld_fp(r.y, f12 + (2 * k + 1) * 10);

@@ -19,7 +19,7 @@ __device__ uint64_t g_diag[4096 * 16];
 template <int TEAMS>
 __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const LineCoef* tab,
                                                const PointG1* hpt, int32_t* codes) {
-  __shared__ uint32_t lds[TEAMS * kTeamWords];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
   Team T = make_team(lds, kTeamWords);
   uint32_t* F = team_regs(T);
   int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);

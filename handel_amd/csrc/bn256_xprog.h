@@ -119,10 +119,11 @@ HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t 
   x_for<NT>([&](auto t) {
     const uint32_t off = x_term_off(w, base + t);
     const int32_t c = x_coef(w, base + t);
-    const uint32_t* x = x_at(T, off);
+    Fp x;
+    ld_fp_a8(x, x_at(T, off));
     if constexpr (K < 0) negk += c < 0 ? (uint32_t)-c : 0u;
 #pragma unroll
-    for (int l = 0; l < 10; l++) acc[l] += (uint32_t)c * x[l];
+    for (int l = 0; l < 10; l++) acc[l] += (uint32_t)c * x.l[l];
   });
 #pragma unroll
   for (int l = 0; l < 10; l++) out[l] = K >= 0 ? acc[l] : acc[l] + negk * kP2N[l];
@@ -158,13 +159,13 @@ template <int W, int NP>
 HG_DEV void x_products(const Team& T, const uint32_t (&w)[W], int base, Acc& acc) {
   if constexpr (NP > 0) {
     Fp a, b;
-    ld_fp(a, x_at(T, x_off(w, base)));
-    ld_fp(b, x_at(T, x_off(w, base + 1)));
+    ld_fp_a8(a, x_at(T, x_off(w, base)));
+    ld_fp_a8(b, x_at(T, x_off(w, base + 1)));
     x_for<NP>([&](auto p) {
       Fp a2, b2;
       if constexpr (p + 1 < NP) {
-        ld_fp(a2, x_at(T, x_off(w, base + 2 * (p + 1))));
-        ld_fp(b2, x_at(T, x_off(w, base + 2 * (p + 1) + 1)));
+        ld_fp_a8(a2, x_at(T, x_off(w, base + 2 * (p + 1))));
+        ld_fp_a8(b2, x_at(T, x_off(w, base + 2 * (p + 1) + 1)));
       }
       acc_mad_pinned(acc, a, b);
       // pin the columns here: the mads of product p stay in this region
@@ -212,11 +213,7 @@ HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
       const uint32_t dst = x_off(w, base);
       uint32_t val[10];
       x_lincomb<W, NT, KP>(T, w, base + 1, val);
-      if (dst != 0xffffu) {
-        uint32_t* o = x_at(T, dst);
-#pragma unroll
-        for (int l = 0; l < 10; l++) o[l] = val[l];
-      }
+      if (dst != 0xffffu) st_fp_a8(x_at(T, dst), val);
     });
     team_sync();
   }
@@ -229,11 +226,11 @@ HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
     uint32_t dst2;
     x_job<W, NP2, NL2, KL2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
     team_sync();
-    if (dst != 0xffffu) st_fp(x_at(T, dst), r);
-    if (dst2 != 0xffffu) st_fp(x_at(T, dst2), r2);
+    if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
+    if (dst2 != 0xffffu) st_fp_a8(x_at(T, dst2), r2.l);
   } else {
     team_sync();
-    if (dst != 0xffffu) st_fp(x_at(T, dst), r);
+    if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
   }
   team_sync();
 }

@@ -32,7 +32,7 @@ HG_DEV void fill(uint32_t* lds, int words, uint32_t seed) {
 
 template <int OP>
 __global__ __launch_bounds__(64) void k_op(uint32_t seed, uint32_t* sink) {
-  __shared__ uint32_t lds[kTeamsPerBlock * kTeamWords];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeamsPerBlock * kTeamWords];
   fill(lds, kTeamsPerBlock * kTeamWords, seed + blockIdx.x);
   Team T = make_team(lds, kTeamWords);
   uint32_t* F = team_regs(T);
