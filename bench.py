@@ -46,10 +46,11 @@ G1_GEN_BYTES = (1).to_bytes(32, "big") + (P - 2).to_bytes(32, "big")
 FPMUL_PER_CHECK = 25271
 # u32 x u32 multiply-adds per Fp multiplication (8-limb CIOS: 2*8^2 + 8)
 MADS_PER_FPMUL = 136
-# Peak v_mad_u64_u32 rate, measured by tools/intrate.hip on MI355X
-# (profiles/r01_intrate.jsonl; half the VALU rate: 256 CU x 4 SIMD x 32 lanes
-# x 2.4 GHz / 2 = 39.3 T/s spec-derived).
-P_MAD_TOPS = 33.19
+# Peak v_mad_u64_u32 rate, measured by tools/intrate.hip on MI355X with 8
+# waves per SIMD (profiles/r01_intrate.jsonl: 34.95 T/s, the highest of the
+# round's runs; half the VALU rate: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 =
+# 39.3 T/s spec-derived).
+P_MAD_TOPS = 34.95
 
 
 def seeded_scalars(n: int, seed: int) -> bytes:
