@@ -430,6 +430,117 @@ __global__ __launch_bounds__(1024) void k_agg_order(int n, const int* keys, int*
   for (int r = tid; r < n; r += blockDim.x) order[atomicAdd(&start[keys[r]], 1)] = r;
 }
 
+// Cooperative Jacobian addition for the fold's LDS tree: the two lanes of a
+// pair (the survivor, side A, and its partner, side B) each load BOTH partials
+// (P = own, Q = partner's) and run ONE instruction stream on different data,
+// so the add-2007-bl formula of g2_add costs each lane 9 Fp2 products instead
+// of 16 (the tree's log2(L) sequential additions are the fold's critical path):
+//   phase 1: zz = P.z^2, u = Q.x zz, s = Q.y (P.z zz)
+//            side A: (Z1Z1, U2, S2), side B: (Z2Z2, U1, S1); swap through LDS;
+//   phase 2: I = (2H)^2, J = H I (both), then the same three products on
+//            selected operands — A: V = U1 I, (2r)^2, 2r (V - X3);
+//            B: S1 J, (Z1 + Z2)^2, ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H = Z3 —
+//            and B hands (S1 J, Z3) to A. Same formulas and field operations
+//            as g2_add, so the survivor's result equals g2_add(P, Q).
+// xo / xp: this lane's and the partner's 6-Fp2 exchange slots. Infinity and
+// H = 0 (doubling or P = -Q) take g2_add's branches on both lanes alike.
+HG_DEV void f2_st(uint32_t* p, const Fp2& a) {  // p 8-byte aligned: 64-bit LDS stores
+  uint64_t* q = (uint64_t*)__builtin_assume_aligned(p, 8);
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    q[i] = (uint64_t)a.x.l[2 * i] | ((uint64_t)a.x.l[2 * i + 1] << 32);
+    q[5 + i] = (uint64_t)a.y.l[2 * i] | ((uint64_t)a.y.l[2 * i + 1] << 32);
+  }
+}
+HG_DEV void f2_ld(Fp2& a, const uint32_t* p) {
+  const uint64_t* q = (const uint64_t*)__builtin_assume_aligned(p, 8);
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint64_t vx = q[i], vy = q[5 + i];
+    a.x.l[2 * i] = (uint32_t)vx;
+    a.x.l[2 * i + 1] = (uint32_t)(vx >> 32);
+    a.y.l[2 * i] = (uint32_t)vy;
+    a.y.l[2 * i + 1] = (uint32_t)(vy >> 32);
+  }
+}
+HG_DEV void f2_pick(Fp2& r, bool c, const Fp2& a, const Fp2& b) { f2_sel(r, c, a, b); }
+HG_DEV void g2_add_pair(G2J& r, const G2J& P, const G2J& Q, bool side_a, uint32_t* xo, const uint32_t* xp) {
+  if (g2_is_inf(P)) {
+    r = Q;
+    return;
+  }
+  if (g2_is_inf(Q)) {
+    r = P;
+    return;
+  }
+  Fp2 zz, u, s, t;
+  f2_sqr(zz, P.z);
+  f2_mul(u, Q.x, zz);
+  f2_mul(t, P.z, zz);
+  f2_mul(s, Q.y, t);
+  f2_st(xo, zz);
+  f2_st(xo + 20, u);
+  f2_st(xo + 40, s);
+  __syncthreads();
+  Fp2 zz2, u2, s2;
+  f2_ld(zz2, xp);
+  f2_ld(u2, xp + 20);
+  f2_ld(s2, xp + 40);
+  __syncthreads();
+  Fp2 z1z1, z2z2, U1, U2, S1, S2;
+  f2_pick(z1z1, side_a, zz, zz2);
+  f2_pick(z2z2, side_a, zz2, zz);
+  f2_pick(U2, side_a, u, u2);
+  f2_pick(U1, side_a, u2, u);
+  f2_pick(S2, side_a, s, s2);
+  f2_pick(S1, side_a, s2, s);
+  Fp2 h, rr;
+  f2_sub(h, U2, U1);
+  f2_sub(rr, S2, S1);
+  if (f2_is_zero(h)) {
+    if (f2_is_zero(rr)) g2_double(r, P);  // P == Q as points
+    else g2_set_inf(r);
+    return;
+  }
+  Fp2 i, j, m1, m2, m3, x3, y2, zs;
+  f2_dbl(t, h);
+  f2_sqr(i, t);
+  f2_mul(j, h, i);
+  f2_dbl(rr, rr);
+  // A: V = U1 I; B: S1 J
+  Fp2 o1, o2;
+  f2_pick(o1, side_a, U1, S1);
+  f2_pick(o2, side_a, i, j);
+  f2_mul(m1, o1, o2);
+  // A: (2r)^2; B: (Z1 + Z2)^2
+  f2_add(zs, P.z, Q.z);
+  f2_pick(o1, side_a, rr, zs);
+  f2_sqr(m2, o1);
+  // A: X3 = (2r)^2 - J - 2V, y2 = V - X3; B: y2 = (Z1 + Z2)^2 - Z1Z1 - Z2Z2
+  f2_sub(x3, m2, j);
+  f2_sub(x3, x3, m1);
+  f2_sub(x3, x3, m1);
+  Fp2 ya, yb;
+  f2_sub(ya, m1, x3);
+  f2_sub(yb, m2, z1z1);
+  f2_sub(yb, yb, z2z2);
+  f2_pick(y2, side_a, ya, yb);
+  // A: 2r (V - X3); B: Z3
+  f2_pick(o1, side_a, rr, h);
+  f2_mul(m3, o1, y2);
+  f2_st(xo, m1);
+  f2_st(xo + 20, m3);
+  __syncthreads();
+  Fp2 s1j, z3;
+  f2_ld(s1j, xp);
+  f2_ld(z3, xp + 20);
+  __syncthreads();
+  f2_dbl(s1j, s1j);
+  r.x = x3;
+  f2_sub(r.y, m3, s1j);
+  r.z = z3;
+}
+
 // One wave per task: 64 / L requests of the same lane count L, one group of L
 // lanes each. Per group: compaction of the nonzero window bytes of the folded
 // mask (one registry-aligned word = 8 windows per lane and pass, segmented
@@ -439,6 +550,7 @@ __global__ __launch_bounds__(64) void k_aggregate(const PointG2* wsum, const Agg
                                                   const uint64_t* words, const int* order, const AggPlan* plans,
                                                   const AggSched* sched, AggPartial* partial) {
   __shared__ G2J part[64];
+  __shared__ __attribute__((aligned(16))) uint32_t xch[64 * 60];  // g2_add_pair exchange slots
   __shared__ uint32_t pos[kAggPosCap];
   __shared__ uint32_t cnt_lds[64];
   __shared__ uint32_t nw_lds[64];
@@ -502,12 +614,16 @@ __global__ __launch_bounds__(64) void k_aggregate(const PointG2* wsum, const Agg
   part[lane] = acc;
   __syncthreads();
   for (int s2 = L / 2; s2 > 0; s2 >>= 1) {
-    if (l < s2) {
-      G2J o = part[lane + s2];
-      G2J mm = part[lane];
-      g2_add(mm, mm, o);
-      part[lane] = mm;
-    }
+    // pairs (l, l + s2) add cooperatively; the other lanes pair with
+    // themselves and discard the result (one instruction stream per wave)
+    const bool side_a = l < s2;
+    const int partner = side_a ? lane + s2 : (l < 2 * s2 ? lane - s2 : lane);
+    const G2J P = part[lane];
+    const G2J Q = part[partner];
+    G2J res;
+    g2_add_pair(res, P, Q, side_a, xch + lane * 60, xch + partner * 60);
+    __syncthreads();
+    if (side_a) part[lane] = res;
     __syncthreads();
   }
   if (has && l == 0) {
