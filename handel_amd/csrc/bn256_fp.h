@@ -90,6 +90,33 @@ HG_DEV void fp_csub(Fp& r, const uint32_t* x) {
   for (int i = 0; i < 10; i++) r.l[i] = keep ? x[i] : s[i];
 }
 
+// fp_csub for REDC outputs: x >= p implies x9 >= p9, and a REDC output of a
+// lazy sum is below p + T/R with T/R far below 2^234, so x9 >= p9 happens for
+// about one lane in 2^22. The subtraction runs under that (exact) test, so the
+// wave normally skips it with one compare and a branch instead of a 10-limb
+// borrow chain and 10 selects — at one wave per SIMD every instruction counts.
+HG_DEV void fp_csub_rare(Fp& r, const uint32_t* x) {
+  uint32_t v[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) v[i] = x[i];
+  if (__builtin_expect(x[9] >= p_top_limb(), 0)) {
+    uint32_t s[10];
+    int32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      int32_t t = (int32_t)x[i] - (int32_t)p_limb(i) - br;
+      br = (t >> 31) & 1;
+      s[i] = (uint32_t)t & kMask;
+    }
+    if (br == 0) {
+#pragma unroll
+      for (int i = 0; i < 10; i++) v[i] = s[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.l[i] = v[i];
+}
+
 // ---------------------------------------------------------------- accumulators
 HG_DEV void acc_zero(Acc& a) {
 #pragma unroll
@@ -136,7 +163,7 @@ HG_DEV void acc_reduce(Fp& r, Acc& a) {
     x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
     carry = v >> 26;
   }
-  fp_csub(r, x);
+  fp_csub_rare(r, x);
 }
 
 HG_DEV void fp_mul(Fp& r, const Fp& a, const Fp& b) {

@@ -25,6 +25,12 @@ def test_fp_mul_matches_bigint(engine):
     def words(xs):
         return np.array([[(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)] for x in xs], dtype=np.uint32)
 
+    # products whose canonical REDC output has the top 26-bit limb of p (the
+    # guarded conditional subtraction's branch is taken and must keep them)
+    top = (O.P >> 234) << 234
+    edge = [O.P - 1, O.P - 2, O.P - 12345, top, top + 1, top + (1 << 233), O.P - (1 << 200)]
+    a_int += edge + [(c * pow(3, -1, O.P)) % O.P for c in edge]
+    b_int += [1] * len(edge) + [3] * len(edge)
     out = engine.fp_mul(words(a_int), words(b_int))
     got = [sum(int(w) << (32 * i) for i, w in enumerate(row)) for row in out]
     want = [(x * y) % O.P for x, y in zip(a_int, b_int)]
