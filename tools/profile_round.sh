@@ -8,7 +8,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$R
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-B="bench.py --steps 5 --warmup 2 --no-cpu"
+B="bench.py --steps 5 --warmup 2 --no-cpu --pipeline 1"
 timeout -k 10 300 python3 $B > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run -- python3 $B > $OUT/ktrace.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_verify -d $OUT/fetch -o run -- python3 $B > $OUT/fetch.log 2>&1 &&
