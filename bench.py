@@ -211,18 +211,21 @@ def main():
     d_sigs = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
     d_codes = torch.zeros(n, dtype=torch.int32, device=dev)
     gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev) for _ in range(world)]
+    d_bits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     def step():
         eng.verify_batch_device(d_pks.data_ptr(), d_sigs.data_ptr(), n, d_codes.data_ptr(), stream.cuda_stream)
         # verdict bitset (bit i = check i valid), gathered over RCCL: the only cross-GPU traffic
-        gather_verdicts(pack_verdicts(d_codes).to(coll_dev), world, gathered)
+        eng.pack_verdicts_device(d_codes.data_ptr(), n, d_bits.data_ptr(), stream.cuda_stream)
+        gather_verdicts(d_bits.to(coll_dev), world, gathered)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     got = d_codes.cpu().numpy()
     assert np.array_equal(got, expect), f"GPU verdicts differ from the expected pattern: {np.flatnonzero(got != expect)[:8]}"
+    assert torch.equal(d_bits, pack_verdicts(d_codes)), "HIP verdict bitset differs from the codes"
 
     eng.timing_enable(True)
     eng.timing_read()

@@ -47,6 +47,7 @@ SIGNATURES = {
     "hg_set_message": (_I, [_P, _P, _SZ]),
     "hg_verify_batch": (_I, [_P, _P, _P, _SZ, _P]),
     "hg_verify_batch_device": (_I, [_P, _P, _P, _SZ, _P, _P]),
+    "hg_pack_verdicts_device": (_I, [_P, _P, _SZ, _P, _P]),
     "hg_verify_aggregate": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P, _P]),
     "hg_verify_aggregate_device": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
     "hg_aggregate_pk": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P]),

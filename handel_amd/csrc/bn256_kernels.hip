@@ -718,6 +718,18 @@ __global__ __launch_bounds__(64) void k_merge_codes(const int32_t* a, const int3
   // pk decode errors win over sig decode errors (the registry is decoded first)
   out[i] = a[i] != HG_OK ? a[i] : b[i];
 }
+// Verdict bitset (the one buffer distributed.py gathers across GPUs): bit j of
+// byte b = check 8b + j passed (code 0); one thread per byte, tail bits 0.
+__global__ __launch_bounds__(64) void k_pack_verdicts(const int32_t* codes, int n, uint8_t* bits) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= (n + 7) / 8) return;
+  uint32_t v = 0;
+  const int base = 8 * b;
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+    if (base + j < n && codes[base + j] == HG_OK) v |= 1u << j;
+  bits[b] = (uint8_t)v;
+}
 __global__ __launch_bounds__(64) void k_sig_into_checks(const PointG1* sigs, int n, CheckIn* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -802,6 +814,9 @@ void launch_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, C
 }
 void launch_merge_codes(const int32_t* a, const int32_t* b, int n, int32_t* out, hipStream_t s) {
   if (n > 0) k_merge_codes<<<nblk(n, 64), 64, 0, s>>>(a, b, n, out);
+}
+void launch_pack_verdicts(const int32_t* codes, int n, uint8_t* bits, hipStream_t s) {
+  if (n > 0) k_pack_verdicts<<<nblk((n + 7) / 8, 64), 64, 0, s>>>(codes, n, bits);
 }
 void launch_sig_into_checks(const PointG1* sigs, int n, CheckIn* out, hipStream_t s) {
   if (n > 0) k_sig_into_checks<<<nblk(n, 64), 64, 0, s>>>(sigs, n, out);

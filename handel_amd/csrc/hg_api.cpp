@@ -397,6 +397,15 @@ int hg_verify_batch_device(hg_ctx* c, const uint8_t* d_pks, const uint8_t* d_sig
   return verify_batch_device_locked(c, d_pks, d_sigs, n, d_codes, s);
 }
 
+int hg_pack_verdicts_device(hg_ctx* c, const int32_t* d_codes, size_t n, uint8_t* d_bits, void* stream) {
+  if (!c || (n && (!d_codes || !d_bits)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  launch_pack_verdicts(d_codes, (int)n, d_bits, stream ? (hipStream_t)stream : c->stream);
+  return check_launch(c);
+}
+
 int hg_verify_batch(hg_ctx* c, const uint8_t* pks, const uint8_t* sigs, size_t n, int32_t* codes) {
   if (!c || (n && (!pks || !sigs || !codes))) return HG_ERR_ARG;
   if (n == 0) return HG_OK;

@@ -100,6 +100,12 @@ class Engine:
         self._check(self.L.hg_verify_batch_device(self.ctx, d_pks, d_sigs, n, d_codes, stream or None),
                     "hg_verify_batch_device")
 
+    def pack_verdicts_device(self, d_codes: int, n: int, d_bits: int, stream: int = 0):
+        """Device verdict bitset (hg_pack_verdicts_device): ceil(n/8) bytes,
+        bit j of byte b = check 8b+j passed."""
+        self._check(self.L.hg_pack_verdicts_device(self.ctx, d_codes, n, d_bits, stream or None),
+                    "hg_pack_verdicts_device")
+
     def verify_aggregate(self, reqs: np.ndarray, words: np.ndarray, sigs: bytes, want_agg: bool = False):
         reqs = np.ascontiguousarray(reqs, dtype=REQ_DTYPE)
         words = np.ascontiguousarray(words, dtype=np.uint64)

@@ -90,6 +90,12 @@ int hg_verify_batch(hg_ctx* ctx, const uint8_t* pks, const uint8_t* sigs, size_t
 int hg_verify_batch_device(hg_ctx* ctx, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n, int32_t* d_codes,
                            void* stream);
 
+/* Verdict bitset of n device-resident codes: bit j of byte b (LSB first) = 1
+ * iff check 8b+j returned HG_OK; ceil(n/8) bytes, tail bits 0. Replaces the
+ * per-check `err == nil` branch of verifyAndPublish (processing.go:270-287)
+ * with the buffer the multi-GPU gather exchanges. Asynchronous on `stream`. */
+int hg_pack_verdicts_device(hg_ctx* ctx, const int32_t* d_codes, size_t n, uint8_t* d_bits, void* stream);
+
 /* n aggregate checks against the registry: the Combine fold over the set
  * bits of each request's level range, then VerifySignature
  * (processing.go:342-368; crypto.go:120-137 for a full-registry request).

@@ -317,3 +317,22 @@ def test_full_size_aggregate_matches_oracle(engine, full):
                                         want_agg=True)
     assert np.array_equal(codes, want)
     assert agg == want_agg
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 4100])
+def test_pack_verdicts_matches_codes(engine, n):
+    """hg_pack_verdicts_device: bit j of byte b = (code[8b+j] == 0), tail bits 0;
+    the same bytes as the torch restatement in handel_amd/distributed.py."""
+    import torch
+
+    from handel_amd.distributed import pack_verdicts
+
+    rng = np.random.default_rng(n)
+    codes = rng.choice(np.array([0, 0, 0, 1, 2, 3, 6], dtype=np.int32), size=n)
+    d_codes = torch.from_numpy(codes).cuda()
+    d_bits = torch.full(((n + 7) // 8,), 0xA5, dtype=torch.uint8, device="cuda")
+    engine.pack_verdicts_device(d_codes.data_ptr(), n, d_bits.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = np.packbits(np.concatenate([codes == 0, np.zeros((-n) % 8, bool)]), bitorder="little")
+    assert np.array_equal(d_bits.cpu().numpy(), want)
+    assert torch.equal(d_bits, pack_verdicts(d_codes))
