@@ -24,12 +24,8 @@ namespace hg {
 //                  all-zero => infinity; else must be on the curve.
 //   cf (cloudflare): each coordinate must be < p; all-zero => infinity; on
 //                  the curve; G2 additionally in the order-n subgroup.
-__global__ __launch_bounds__(64) void k_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int32_t* codes) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t* m = bytes + (size_t)i * 128;
+HG_DEV int32_t decode_g2_one(const uint8_t* m, int flavor, PointG2& P) {
   bool ge[4];
-  PointG2 P;
   fp_from_be(P.x.x, m, &ge[0]);
   fp_from_be(P.x.y, m + 32, &ge[1]);
   fp_from_be(P.y.x, m + 64, &ge[2]);
@@ -54,16 +50,11 @@ __global__ __launch_bounds__(64) void k_decode_g2(const uint8_t* bytes, int n, i
       if (!g2_is_inf(r)) code = HG_ERR_CF_MALFORMED;
     }
   }
-  out[i] = P;
-  codes[i] = code;
+  return code;
 }
 
-__global__ __launch_bounds__(64) void k_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t* m = bytes + (size_t)i * 64;
+HG_DEV int32_t decode_g1_one(const uint8_t* m, int flavor, PointG1& P) {
   bool gx, gy;
-  PointG1 P;
   fp_from_be(P.x, m, &gx);
   fp_from_be(P.y, m + 32, &gy);
   bool nz = false;
@@ -75,8 +66,41 @@ __global__ __launch_bounds__(64) void k_decode_g1(const uint8_t* bytes, int n, i
   } else if (nz && !g1_on_curve(P.x, P.y)) {
     code = flavor == HG_FLAVOR_CF ? HG_ERR_CF_MALFORMED : HG_ERR_SIG_UNMARSHAL;
   }
+  return code;
+}
+
+__global__ __launch_bounds__(64) void k_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int32_t* codes) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  PointG2 P;
+  const int32_t code = decode_g2_one(bytes + (size_t)i * 128, flavor, P);
   out[i] = P;
   codes[i] = code;
+}
+
+__global__ __launch_bounds__(64) void k_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  PointG1 P;
+  const int32_t code = decode_g1_one(bytes + (size_t)i * 64, flavor, P);
+  out[i] = P;
+  codes[i] = code;
+}
+
+// The pairing-check inputs in one pass (hg_verify_batch*): pk and sig decoded
+// by the same thread straight into CheckIn, pk errors before sig errors (the
+// order PublicKey.UnmarshalBinary / SigBLS unmarshal surface them).
+__global__ __launch_bounds__(64) void k_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor,
+                                                     CheckIn* out, int32_t* codes) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  PointG2 Q;
+  PointG1 S;
+  const int32_t a = decode_g2_one(pks + (size_t)i * 128, flavor, Q);
+  const int32_t b = decode_g1_one(sigs + (size_t)i * 64, flavor, S);
+  out[i].pk = Q;
+  out[i].sig = S;
+  codes[i] = a != HG_OK ? a : b;
 }
 
 // ------------------------------------------------------------------ encode
@@ -767,6 +791,10 @@ void launch_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int
 }
 void launch_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes, hipStream_t s) {
   if (n > 0) k_decode_g1<<<nblk(n, 64), 64, 0, s>>>(bytes, n, flavor, out, codes);
+}
+void launch_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor, CheckIn* out, int32_t* codes,
+                          hipStream_t s) {
+  if (n > 0) k_decode_checks<<<nblk(n, 64), 64, 0, s>>>(pks, sigs, n, flavor, out, codes);
 }
 void launch_encode_g2(const PointG2* in, int n, uint8_t* out, hipStream_t s) {
   if (n > 0) k_encode_g2<<<nblk(n, 64), 64, 0, s>>>(in, n, out);

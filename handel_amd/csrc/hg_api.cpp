@@ -370,19 +370,12 @@ static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uin
     c->err = "hg_set_message was not called";
     return HG_ERR_ARG;
   }
-  HG_CHECK(c, c->pts2.ensure(n));
-  HG_CHECK(c, c->pts1.ensure(n));
   HG_CHECK(c, c->checks.ensure(n));
-  HG_CHECK(c, c->codes_a.ensure(n));
-  HG_CHECK(c, c->codes_b.ensure(n));
-  launch_decode_g2(d_pks, (int)n, c->flavor, c->pts2.p, c->codes_a.p, s);
-  launch_decode_g1(d_sigs, (int)n, c->flavor, c->pts1.p, c->codes_b.p, s);
-  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, d_codes, s);
+  launch_decode_checks(d_pks, d_sigs, (int)n, c->flavor, c->checks.p, d_codes, s);
   if (c->hash_eof) {
     k_fill_codes<<<nb(n), 256, 0, s>>>(d_codes, (int)n, HG_OK, HG_ERR_HASH_EOF);
     return check_launch(c);
   }
-  launch_checks_from_points(c->pts2.p, c->pts1.p, (int)n, c->checks.p, s);
   timed_verify(c, c->checks.p, (int)n, d_codes, s);
   return check_launch(c);
 }
