@@ -87,20 +87,31 @@ __global__ __launch_bounds__(64) void k_decode_g1(const uint8_t* bytes, int n, i
   codes[i] = code;
 }
 
-// The pairing-check inputs in one pass (hg_verify_batch*): pk and sig decoded
-// by the same thread straight into CheckIn, pk errors before sig errors (the
-// order PublicKey.UnmarshalBinary / SigBLS unmarshal surface them).
-__global__ __launch_bounds__(64) void k_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor,
-                                                     CheckIn* out, int32_t* codes) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  PointG2 Q;
-  PointG1 S;
-  const int32_t a = decode_g2_one(pks + (size_t)i * 128, flavor, Q);
-  const int32_t b = decode_g1_one(sigs + (size_t)i * 64, flavor, S);
-  out[i].pk = Q;
-  out[i].sig = S;
-  codes[i] = a != HG_OK ? a : b;
+// The pairing-check inputs in one pass (hg_verify_batch*): 64 checks per
+// 128-thread block, wave 0 decodes the pks and wave 1 the sigs (the two run
+// side by side instead of one after the other), straight into CheckIn; pk
+// errors before sig errors (the order PublicKey.UnmarshalBinary / SigBLS
+// unmarshal surface them).
+__global__ __launch_bounds__(128) void k_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor,
+                                                      CheckIn* out, int32_t* codes) {
+  __shared__ int32_t sig_code[64];
+  const int l = threadIdx.x & 63;
+  const int i = blockIdx.x * 64 + l;
+  const bool pk_wave = threadIdx.x < 64;  // wave-uniform
+  int32_t a = HG_OK;
+  if (i < n) {
+    if (pk_wave) {
+      PointG2 Q;
+      a = decode_g2_one(pks + (size_t)i * 128, flavor, Q);
+      out[i].pk = Q;
+    } else {
+      PointG1 S;
+      sig_code[l] = decode_g1_one(sigs + (size_t)i * 64, flavor, S);
+      out[i].sig = S;
+    }
+  }
+  __syncthreads();
+  if (pk_wave && i < n) codes[i] = a != HG_OK ? a : sig_code[l];
 }
 
 // ------------------------------------------------------------------ encode
@@ -794,7 +805,7 @@ void launch_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int
 }
 void launch_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor, CheckIn* out, int32_t* codes,
                           hipStream_t s) {
-  if (n > 0) k_decode_checks<<<nblk(n, 64), 64, 0, s>>>(pks, sigs, n, flavor, out, codes);
+  if (n > 0) k_decode_checks<<<nblk(n, 64), 128, 0, s>>>(pks, sigs, n, flavor, out, codes);
 }
 void launch_encode_g2(const PointG2* in, int n, uint8_t* out, hipStream_t s) {
   if (n > 0) k_encode_g2<<<nblk(n, 64), 64, 0, s>>>(in, n, out);
