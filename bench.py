@@ -1,17 +1,28 @@
 #!/usr/bin/env python3
-"""Headline benchmark: BN256 BLS verifications/s at batch 4096 on MI355X.
+"""Headline benchmark: BN256 aggregate-signature verifications/s at batch 4096.
 
-Workload (BASELINE.json configs[1]): one step =
-4096 independent PublicKey.VerifySignature(lib.Message, sig) checks
-(bn256/go/bn256.go:82-94) with 1/8 of the signatures tampered, inputs
-(marshalled pks and sigs) already resident in HBM, verdict codes written
-back to HBM, then the verdict bitset gathered to rank 0 over RCCL.
-Keys/signatures are synthetic (seeded scalars, keygen/sign on the GPU).
+Headline workload (BASELINE.json configs[2]): one
+step = 4096 incoming Handel multisignatures verified against a 4000-key
+registry resident on the GPU, as processing.go:342-368 verifySignature does
+for each of them — the bitset-driven PublicKey.Combine fold over the level's
+registry range, then PublicKey.VerifySignature (bn256/go/bn256.go:82-94).
+Requests are a random node's random Handel level (partitioner rangeLevel), a
+bitset of density U[0.5, 1], the aggregate signature of the set bits, 1/8 of
+the aggregates tampered. Inputs (requests, bitset words, signatures) are
+resident in HBM; verdict codes are written to HBM, packed into a bitset and
+all-gathered over RCCL (the only cross-GPU traffic).
+
+Sub-lines (never `value`):
+  single          config 2: 4096 independent single-signature checks
+                  (simul/p2p/aggregator.go:244 verifyPacket)
+  full_registry   config 3's VerifyMultiSignature shape: every request spans
+                  the whole registry (crypto.go:120-137)
+  pipelined       two headline batches in flight on two HIP streams
+--committees switches the headline to config 5: each rank is one committee of
+4096 signers (its own 4096-key registry) verifying 4096 multisignatures.
 
 Multi-GPU: one process per GPU (torchrun), every rank verifies its own batch
-of 4096 (weak scaling, no data-path collective); the only exchange is the
-all_gather of 512-byte verdict bitsets.
-
+(weak scaling); value = all ranks' checks / max-over-ranks wall time.
 Prints ONE JSON line on rank 0.
 """
 
@@ -20,6 +31,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -30,26 +42,27 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+from handel_amd import _lib  # noqa: E402
 from handel_amd.distributed import gather_verdicts, pack_verdicts  # noqa: E402
-from handel_amd.engine import Engine  # noqa: E402
+from handel_amd.engine import REQ_DTYPE, Engine  # noqa: E402
 
 LIB_MESSAGE = b"Everything that is beautiful and noble is the product of reason and calculation."
 ORDER = 65000549695646603732796438742359905742570406053903786389881062969044166799969
 P = 65000549695646603732796438742359905742825358107623003571877145026864184071783
 G1_GEN_BYTES = (1).to_bytes(32, "big") + (P - 2).to_bytes(32, "big")
 
-# Algorithmic work per check, fixed before tuning by the oracle's op counter
-# (oracle/bn256_ref.c, fast=2: one multi-Miller loop over 6u+2 with the pk
-# lines on the fly and the G2Base lines from a table, one final
-# exponentiation, Karatsuba tower formulas): Fp multiplications per check.
-# tests/test_oracle.py pins this number.
+# Algorithmic work, fixed before tuning; tests/test_oracle.py
+# pins FPMUL_PER_CHECK against the oracle's op counter (oracle/bn256_ref.c,
+# fast=2: one multi-Miller loop over 6u+2 with the pk lines on the fly and the
+# G2Base lines from a table, one final exponentiation, Karatsuba tower formulas).
 FPMUL_PER_CHECK = 25271
+# one G2 mixed addition (madd-2007-bl: 7M2 + 4S2, Fp2 products as 3 Fp products)
+FPMUL_PER_G2_ADD = 29
 # u32 x u32 multiply-adds per Fp multiplication (8-limb CIOS: 2*8^2 + 8)
 MADS_PER_FPMUL = 136
 # Peak v_mad_u64_u32 rate, measured by tools/intrate.hip on MI355X with 8
-# waves per SIMD (profiles/r01_intrate.jsonl: 34.95 T/s, the highest of the
-# round's runs; half the VALU rate: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 =
-# 39.3 T/s spec-derived).
+# waves per SIMD (profiles/r01_intrate.jsonl: 34.95 T/s; half the VALU rate:
+# 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 = 39.3 T/s spec-derived).
 P_MAD_TOPS = 34.95
 
 
@@ -64,31 +77,35 @@ def seeded_scalars(n: int, seed: int) -> bytes:
     return bytes(out)
 
 
-def make_batch(eng: Engine, n: int, seed: int):
-    kb = seeded_scalars(n, seed)
-    pks = eng.keygen(kb)
-    sigs = bytearray(eng.sign(kb))
-    # tamper 1/8 of the signatures: sig + G1
+def _tamper(eng: Engine, sigs: bytearray, n: int) -> np.ndarray:
+    """sig + G1 for every 8th signature; expected codes."""
     idx = list(range(0, n, 8))
-    a = b"".join(bytes(sigs[64 * i:64 * i + 64]) for i in idx)
-    bad, codes = eng.combine_g1(a, G1_GEN_BYTES * len(idx))
+    bad, codes = eng.combine_g1(b"".join(bytes(sigs[64 * i:64 * i + 64]) for i in idx), G1_GEN_BYTES * len(idx))
     assert not codes.any()
     for j, i in enumerate(idx):
         sigs[64 * i:64 * i + 64] = bad[64 * j:64 * j + 64]
     expect = np.zeros(n, dtype=np.int32)
     expect[idx] = 1
+    return expect
+
+
+def make_batch(eng: Engine, n: int, seed: int):
+    """Config 2: n independent (pk, sig) pairs on lib.Message, 1/8 tampered."""
+    kb = seeded_scalars(n, seed)
+    pks = eng.keygen(kb)
+    sigs = bytearray(eng.sign(kb))
+    expect = _tamper(eng, sigs, n)
     return pks, bytes(sigs), expect
 
 
 def make_aggregate_batch(eng: Engine, n_reg: int, n: int, seed: int, full: bool = False):
-    """a registry of n_reg keys and n incoming
-    multisignatures as Handel's evaluator receives them: for each, a random
-    node's random non-empty level (partitioner rangeLevel, partitioner.go:133-178),
-    a bitset of density U[0.5, 1.0] over the level's registry range, and the
-    aggregate signature of the set bits (sum of the secret keys times H(msg));
-    1/8 of the aggregates tampered (+ G1). full=True: every request spans the
-    whole registry (crypto.go:120-137 VerifyMultiSignature, config 3's second
-    workload)."""
+    """a registry of n_reg keys (loaded into `eng`)
+    and n incoming multisignatures as Handel's evaluator receives them: for
+    each, a random node's random non-empty level (partitioner rangeLevel,
+    partitioner.go:133-178), a bitset of density U[0.5, 1.0] over the level's
+    registry range, and the aggregate signature of the set bits (sum of the
+    secret keys times H(msg)); 1/8 of the aggregates tampered (+ G1).
+    full=True: every request spans the whole registry (crypto.go:120-137)."""
     from handel_amd.partitioner import bits_to_words, level_sizes
 
     rng = np.random.default_rng(seed)
@@ -114,25 +131,17 @@ def make_aggregate_batch(eng: Engine, n_reg: int, n: int, seed: int, full: bool 
         words.extend(int(x) for x in w)
         scalars += k.to_bytes(32, "big")
     sigs = bytearray(eng.sign(bytes(scalars)))
-    idx = list(range(0, n, 8))
-    bad, codes = eng.combine_g1(b"".join(bytes(sigs[64 * i:64 * i + 64]) for i in idx), G1_GEN_BYTES * len(idx))
-    assert not codes.any()
-    for j, i in enumerate(idx):
-        sigs[64 * i:64 * i + 64] = bad[64 * j:64 * j + 64]
-    expect = np.zeros(n, dtype=np.int32)
-    expect[idx] = 1
-    from handel_amd.engine import REQ_DTYPE
-
-    return np.array(reqs, dtype=REQ_DTYPE), np.array(words, dtype=np.uint64), bytes(sigs), expect, np.array(signers)
+    expect = _tamper(eng, sigs, n)
+    return (np.array(reqs, dtype=REQ_DTYPE), np.array(words, dtype=np.uint64), bytes(sigs), expect,
+            np.array(signers), reg)
 
 
-def pmc_traffic():
-    """HBM bytes per k_verify launch from the newest committed PMC summary
-    (profiles/*_pmc.csv, written by tools/profile_round.sh +
-    tools/rocpd_summary.py): FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE."""
+def pmc_traffic(pattern: str):
+    """HBM bytes per launch of the kernels matching `pattern`, summed, from the
+    newest committed PMC summary (profiles/*_pmc.csv, tools/rocpd_summary.py):
+    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE."""
     import csv
     import glob
-
     import re
 
     # newest = highest round/version in the name (mtimes are not kept by git or the box snapshot)
@@ -144,28 +153,183 @@ def pmc_traffic():
         vals = {}
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "k_verify" in row["kernel"]:
-                    vals[row["counter"]] = float(row["avg"])
+                if re.search(pattern, row["kernel"]):
+                    vals[row["counter"]] = vals.get(row["counter"], 0.0) + float(row["avg"])
         if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
             return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(path, ROOT)
     return None, None
 
 
-def cpu_baseline(n_sample: int, pks: bytes, sigs: bytes, expect: np.ndarray):
-    """The reference algorithm restated in C (oracle/bn256_ref.c, 'port'):
-    two full pairings + GT compare per check, timed on this host's cores."""
+def host_cpu():
+    """(threads to use, description) — the box's CPU share for one GPU is the
+    thread budget (OMP_NUM_THREADS / the affinity mask), nproc and the model
+    are reported beside it."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(aff, omp) if omp > 0 else aff
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:  # pragma: no cover
+        pass
+    return threads, {"nproc": os.cpu_count(), "affinity": aff, "model": model}
+
+
+def cpu_baseline_single(pks: bytes, sigs: bytes, expect: np.ndarray):
+    """Config 2 on the reference algorithm restated in C (oracle/bn256_ref.c,
+    'port'): two full pairings + GT compare per check."""
     from oracle import ref_lib as R
 
-    threads = min(16, os.cpu_count() or 1)
-    reps = 3  # ~25 s of CPU work on 16 threads at the measured ~8k checks/s
+    threads, info = host_cpu()
+    n = len(expect)
     t0 = time.perf_counter()
-    for _ in range(reps):
-        codes = R.verify_batch(LIB_MESSAGE, pks[:128 * n_sample], sigs[:64 * n_sample], nthreads=threads, fast=0)
-        assert np.array_equal(codes, expect[:n_sample]), "CPU oracle verdicts differ"
+    codes = R.verify_batch(LIB_MESSAGE, pks, sigs, nthreads=threads, fast=0)
     dt = time.perf_counter() - t0
-    return {"value": round(reps * n_sample / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} passes over {n_sample} checks of the same batch (lib.Message, 1/8 tampered), "
-                      f"reference algorithm (2 pairings + GT compare), {threads} threads, {dt:.2f} s wall"}
+    assert np.array_equal(codes, expect), "CPU oracle verdicts differ"
+    return {"value": round(n / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
+            "per_core": round(n / dt / threads, 1), **info,
+            "sample": f"the same {n} checks (lib.Message, 1/8 tampered), reference algorithm "
+                      f"(2 pairings + GT compare per check), {threads} threads, {dt:.2f} s wall"}
+
+
+def cpu_baseline_aggregate(reg: bytes, reqs, words, sigs: bytes, expect: np.ndarray, n_sample: int):
+    """Config 3 on the reference algorithm restated in C: per request the
+    PublicKey.Combine fold over every set bit (one G2 addition each, as
+    processing.go:355-363), then two pairings + GT compare."""
+    from oracle import ref_lib as R
+
+    threads, info = host_cpu()
+    m = min(n_sample, len(reqs))
+    r = reqs[:m]
+    t0 = time.perf_counter()
+    codes = R.verify_aggregate(LIB_MESSAGE, reg, r["offset"], r["bitlen"], r["level_size"], words,
+                               r["word_offset"].astype(np.uint64), sigs[:64 * m], nthreads=threads, fast=0)
+    dt = time.perf_counter() - t0
+    assert np.array_equal(codes, expect[:m]), "CPU oracle verdicts differ"
+    return {"value": round(m / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
+            "per_core": round(m / dt / threads, 1), **info,
+            "sample": f"the first {m} requests of the batch (same registry, bitsets, signatures), reference "
+                      f"algorithm (one G2 addition per set bit + 2 pairings + GT compare), {threads} threads, "
+                      f"{dt:.2f} s wall"}
+
+
+class Timer:
+    """Barrier + synchronize on both sides of the timed region, max over ranks."""
+
+    def __init__(self, dev, dist, coll_dev):
+        self.dev, self.dist, self.coll_dev = dev, dist, coll_dev
+
+    def run(self, step, steps: int, warmup: int) -> float:
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(self.dev)
+        if self.dist:
+            import torch.distributed as tdist
+            tdist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(self.dev)
+        if self.dist:
+            tdist.barrier()
+        dt = time.perf_counter() - t0
+        if self.dist:
+            t = torch.tensor([dt], dtype=torch.float64, device=self.coll_dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+
+def _dev_bytes(b: bytes, dev):
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+
+
+class AggregateWorkload:
+    """Config 3 (or 5): n multisignatures on an n_reg-key registry per rank."""
+
+    def __init__(self, eng: Engine, n_reg: int, n: int, seed: int, dev, stream, full: bool = False):
+        self.eng, self.n, self.stream = eng, n, stream
+        (self.reqs, self.words, self.sigs, self.expect, self.signers,
+         self.reg) = make_aggregate_batch(eng, n_reg, n, seed, full=full)
+        self.d_reqs = _dev_bytes(self.reqs.tobytes(), dev)
+        self.d_words = _dev_bytes(self.words.tobytes(), dev)
+        self.d_sigs = _dev_bytes(self.sigs, dev)
+        self.d_codes = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.d_bits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
+        # algorithmic Fp multiplications of the batch: one G2 addition per set
+        # bit (the reference's fold) + one pairing check per request
+        self.fpmul = int(self.signers.sum()) * FPMUL_PER_G2_ADD + n * FPMUL_PER_CHECK
+
+    def submit(self, eng=None, codes=None, stream=None):
+        eng = self.eng if eng is None else eng
+        codes = self.d_codes if codes is None else codes
+        stream = self.stream if stream is None else stream
+        eng.verify_aggregate_device(self.d_reqs.data_ptr(), self.n, self.d_words.data_ptr(), self.d_sigs.data_ptr(),
+                                    codes.data_ptr(), 0, stream.cuda_stream)
+
+    def pack(self):
+        self.eng.pack_verdicts_device(self.d_codes.data_ptr(), self.n, self.d_bits.data_ptr(), self.stream.cuda_stream)
+
+    def check(self, codes=None):
+        got = (codes if codes is not None else self.d_codes).cpu().numpy()
+        assert np.array_equal(got, self.expect), \
+            f"GPU verdicts differ from the expected pattern at {np.flatnonzero(got != self.expect)[:8]}"
+
+
+class SingleWorkload:
+    """Config 2: n independent single-signature checks per rank."""
+
+    def __init__(self, eng: Engine, n: int, seed: int, dev, stream):
+        self.eng, self.n, self.stream = eng, n, stream
+        self.pks, self.sigs, self.expect = make_batch(eng, n, seed)
+        self.d_pks = _dev_bytes(self.pks, dev)
+        self.d_sigs = _dev_bytes(self.sigs, dev)
+        self.d_codes = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.d_bits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
+        self.fpmul = n * FPMUL_PER_CHECK
+
+    def submit(self):
+        self.eng.verify_batch_device(self.d_pks.data_ptr(), self.d_sigs.data_ptr(), self.n, self.d_codes.data_ptr(),
+                                     self.stream.cuda_stream)
+
+    def pack(self):
+        self.eng.pack_verdicts_device(self.d_codes.data_ptr(), self.n, self.d_bits.data_ptr(), self.stream.cuda_stream)
+
+    def check(self):
+        got = self.d_codes.cpu().numpy()
+        assert np.array_equal(got, self.expect), f"GPU verdicts differ at {np.flatnonzero(got != self.expect)[:8]}"
+
+
+def timed_phases(eng: Engine, run):
+    """Runs run() with the engine's HIP-event timing on; returns per-phase
+    (mean ms per interval) for verify / aggregate fold / whole submission."""
+    eng.timing_enable(True)
+    for ph in (_lib.HG_PHASE_VERIFY, _lib.HG_PHASE_AGGREGATE, _lib.HG_PHASE_SUBMIT):
+        eng.timing_read_phase(ph)
+    run()
+    out = {}
+    for name, ph in (("verify", _lib.HG_PHASE_VERIFY), ("fold", _lib.HG_PHASE_AGGREGATE),
+                     ("submit", _lib.HG_PHASE_SUBMIT)):
+        ms, k = eng.timing_read_phase(ph)
+        out[name] = ms / k if k else None
+    eng.timing_enable(False)
+    return out
+
+
+def roofline(fpmul: int, ms: float, kernel: str, traffic_pattern: str, work: str):
+    achieved = fpmul * MADS_PER_FPMUL / (ms * 1e-3) / 1e12
+    traffic, src = pmc_traffic(traffic_pattern)
+    return {"bound": "valu", "achieved": round(achieved, 3), "peak": P_MAD_TOPS, "unit": "Tmad/s",
+            "frac": round(achieved / P_MAD_TOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+            "traffic_source": src, "kernel": kernel, "kernel_ms": round(ms, 4), "work": work}
 
 
 def main():
@@ -174,10 +338,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--committees", action="store_true",
+                    help="config 5: each rank is one committee of 4096 signers (own 4096-key registry)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-aggregate", action="store_true", help="skip the config-3 aggregate-verify line")
-    ap.add_argument("--pipeline", type=int, default=2,
-                    help="batches in flight for the extra 'pipelined' report (1: skip)")
+    ap.add_argument("--no-extra", action="store_true", help="headline only (no single / full / pipelined lines)")
+    ap.add_argument("--pipeline", type=int, default=2, help="batches in flight for the 'pipelined' line (1: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=4096, help="requests in the CPU baseline's sample")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -202,159 +368,124 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local_dev)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
+    timer = Timer(dev, dist, coll_dev)
+    stream = torch.cuda.current_stream(dev)
+    n = args.batch
 
     eng = Engine(device=local_dev, flavor="go")
     assert eng.set_message(LIB_MESSAGE) == 0
-    n = args.batch
-    pks, sigs, expect = make_batch(eng, n, seed=1234 + rank)
-    d_pks = torch.frombuffer(bytearray(pks), dtype=torch.uint8).to(dev)
-    d_sigs = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
-    d_codes = torch.zeros(n, dtype=torch.int32, device=dev)
+    n_reg = 4096 if args.committees else 4000
+    head = AggregateWorkload(eng, n_reg, n, seed=4321 + rank, dev=dev, stream=stream)
     gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev) for _ in range(world)]
-    d_bits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
 
     def step():
-        eng.verify_batch_device(d_pks.data_ptr(), d_sigs.data_ptr(), n, d_codes.data_ptr(), stream.cuda_stream)
+        head.submit()
         # verdict bitset (bit i = check i valid), gathered over RCCL: the only cross-GPU traffic
-        eng.pack_verdicts_device(d_codes.data_ptr(), n, d_bits.data_ptr(), stream.cuda_stream)
-        gather_verdicts(d_bits.to(coll_dev), world, gathered)
+        head.pack()
+        gather_verdicts(head.d_bits.to(coll_dev), world, gathered)
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize(dev)
-    got = d_codes.cpu().numpy()
-    assert np.array_equal(got, expect), f"GPU verdicts differ from the expected pattern: {np.flatnonzero(got != expect)[:8]}"
-    assert torch.equal(d_bits, pack_verdicts(d_codes)), "HIP verdict bitset differs from the codes"
-
-    eng.timing_enable(True)
-    eng.timing_read()
+    head.check()
+    assert torch.equal(head.d_bits, pack_verdicts(head.d_codes)), "HIP verdict bitset differs from the codes"
+    dt = timer.run(step, args.steps, args.warmup)
+    head.check()
     if dist:
-        tdist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        tdist.barrier()
-    dt = time.perf_counter() - t0
-    kern_ms, launches = eng.timing_read()
-    eng.timing_enable(False)
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t.item())
-    got = d_codes.cpu().numpy()
-    assert np.array_equal(got, expect)
+        want = [pack_verdicts(torch.from_numpy(head.expect))]
+        assert torch.equal(gathered[rank].cpu(), want[0]), "gathered bitset of this rank differs"
+    ph = timed_phases(eng, lambda: [head.submit() for _ in range(5)])
+    value = n * args.steps * world / dt
+    # the dominant kernels of the step: the Combine fold (plan, order, fold,
+    # finish) and the pairing check, on the reference's algorithmic work
+    agg_ms = ph["fold"] + ph["verify"]
+    roof = roofline(head.fpmul, agg_ms, "k_agg_plan + k_agg_order + k_aggregate + k_agg_finish + k_verify",
+                    r"k_agg_|k_aggregate|k_verify",
+                    f"per check: {FPMUL_PER_G2_ADD} Fp-mul per set bit (G2 addition) + {FPMUL_PER_CHECK} "
+                    f"(pairing check), x {MADS_PER_FPMUL} u32 mads; mean {head.signers.mean():.1f} set bits")
+    roof["kernels_ms"] = {"fold": round(ph["fold"], 4), "k_verify": round(ph["verify"], 4),
+                          "submit": round(ph["submit"], 4)}
+    roof_verify = roofline(n * FPMUL_PER_CHECK, ph["verify"], "k_verify", r"k_verify",
+                           f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads per check")
 
-    total = n * args.steps * world
-    value = total / dt
-    avg_kernel_ms = kern_ms / max(launches, 1)
-    achieved = n * FPMUL_PER_CHECK * MADS_PER_FPMUL / (avg_kernel_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic()
-    roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": P_MAD_TOPS, "unit": "Tmad/s",
-                "frac": round(achieved / P_MAD_TOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": traffic_src,
-                "kernel": "k_verify", "kernel_ms": round(avg_kernel_ms, 4),
-                "work_per_check": f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads"}
-    # config 3: aggregate verification of Handel multisignatures on a
-    # 4000-key registry — bitset-driven G2 Combine + pairing check, inputs resident
-    def time_aggregate(full: bool):
-        reqs, words, asigs, aexpect, sizes = make_aggregate_batch(eng, 4000, n, seed=4321 + rank, full=full)
-        d_reqs = torch.frombuffer(bytearray(reqs.tobytes()), dtype=torch.uint8).to(dev)
-        d_words = torch.frombuffer(bytearray(words.tobytes()), dtype=torch.uint8).to(dev)
-        d_asigs = torch.frombuffer(bytearray(asigs), dtype=torch.uint8).to(dev)
-        d_acodes = torch.zeros(n, dtype=torch.int32, device=dev)
+    extra = {}
+    if not args.no_extra:
+        # config 2: independent single-signature checks
+        single = SingleWorkload(eng, n, seed=1234 + rank, dev=dev, stream=stream)
 
-        def astep():
-            eng.verify_aggregate_device(d_reqs.data_ptr(), n, d_words.data_ptr(), d_asigs.data_ptr(),
-                                        d_acodes.data_ptr(), 0, stream.cuda_stream)
+        def sstep():
+            single.submit()
+            single.pack()
+            gather_verdicts(single.d_bits.to(coll_dev), world, gathered)
 
-        for _ in range(args.warmup):
-            astep()
-        torch.cuda.synchronize(dev)
-        assert np.array_equal(d_acodes.cpu().numpy(), aexpect), "aggregate verdicts differ from the expected pattern"
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            astep()
-        torch.cuda.synchronize(dev)
-        if dist:
-            tdist.barrier()
-        adt = time.perf_counter() - t0
-        if dist:
-            t = torch.tensor([adt], dtype=torch.float64, device=coll_dev)
-            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-            adt = float(t.item())
-        assert np.array_equal(d_acodes.cpu().numpy(), aexpect)
-        scope = ("every request spans the whole 4000-key registry (VerifyMultiSignature)" if full else
-                 "random node/level of a 4000-node Handel registry")
-        return {"metric": "BN254 aggregate-sig verifications/sec (Handel multisigs, 4000-key registry)",
-                "value": round(n * args.steps * world / adt, 1), "unit": "verifications/s",
-                "ms_per_step": round(adt / args.steps * 1e3, 4),
-                "workload": f"config 3: {n} multisigs per GPU, {scope}, bitset density U[0.5,1], 1/8 tampered",
-                "signers_per_check_mean": round(float(sizes.mean()), 1),
-                "signers_per_check_max": int(sizes.max())}
+        sdt = timer.run(sstep, args.steps, args.warmup)
+        single.check()
+        sph = timed_phases(eng, lambda: [single.submit() for _ in range(5)])
+        extra["single"] = {
+            "metric": "BN254 single-sig verifications/sec (batch 4096)",
+            "value": round(n * args.steps * world / sdt, 1), "unit": "verifications/s",
+            "ms_per_step": round(sdt / args.steps * 1e3, 4),
+            "workload": f"config 2: {n} independent BLS pairing checks per GPU (lib.Message, 1/8 tampered)",
+            "roofline": roofline(single.fpmul, sph["verify"], "k_verify", r"k_verify",
+                                 f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads per check")}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            try:
+                extra["single"]["cpu_baseline"] = cpu_baseline_single(single.pks, single.sigs, single.expect)
+            except Exception as e:  # pragma: no cover - reported, not fatal
+                extra["single"]["cpu_baseline"] = {"error": str(e)}
+        del single
+        # VerifyMultiSignature shape: every request spans the whole registry
+        full = AggregateWorkload(eng, n_reg, n, seed=8765 + rank, dev=dev, stream=stream, full=True)
+        fdt = timer.run(full.submit, args.steps, args.warmup)
+        full.check()
+        fph = timed_phases(eng, lambda: [full.submit() for _ in range(5)])
+        extra["full_registry"] = {
+            "metric": "BN254 aggregate-sig verifications/sec (VerifyMultiSignature over the registry)",
+            "value": round(n * args.steps * world / fdt, 1), "unit": "verifications/s",
+            "ms_per_step": round(fdt / args.steps * 1e3, 4),
+            "workload": f"{n} multisigs per GPU, every request spans the whole {n_reg}-key registry "
+                        "(crypto.go:120-137), bitset density U[0.5,1], 1/8 tampered",
+            "signers_per_check_mean": round(float(full.signers.mean()), 1),
+            "kernels_ms": {k: round(v, 4) for k, v in fph.items() if v is not None},
+            "roofline": roofline(full.fpmul, fph["fold"] + fph["verify"], "fold + k_verify",
+                                 r"k_agg_|k_aggregate|k_verify", "as the headline")}
+        del full
+        # reload the headline registry (the full-registry workload replaced it)
+        assert not eng.registry_load(head.reg).any()
+        if args.pipeline > 1:
+            # a verifier serving a continuous stream: batches in flight on several
+            # HIP streams, one engine context (own workspaces) per stream
+            engs = [eng] + [Engine(device=local_dev, flavor="go") for _ in range(args.pipeline - 1)]
+            for e in engs[1:]:
+                assert e.set_message(LIB_MESSAGE) == 0
+                assert not e.registry_load(head.reg).any()
+            streams = [stream] + [torch.cuda.Stream(dev) for _ in engs[1:]]
+            codes_p = [head.d_codes] + [torch.zeros(n, dtype=torch.int32, device=dev) for _ in engs[1:]]
 
-    aggregate = aggregate_full = None
-    if not args.no_aggregate:
-        aggregate = time_aggregate(False)
-        aggregate_full = time_aggregate(True)
+            def pstep():
+                for e, st, cd in zip(engs, streams, codes_p):
+                    head.submit(eng=e, codes=cd, stream=st)
 
-    # Pipelined batches (reported beside the headline, never as `value`): a
-    # Handel node verifies a continuous stream of batches, and two 4096-check
-    # batches in flight on two HIP streams (two engine contexts, each with its
-    # own scratch) put two k_verify waves on every SIMD instead of one.
-    pipelined = None
-    if args.pipeline > 1:
-        engs = [eng] + [Engine(device=local_dev, flavor="go") for _ in range(args.pipeline - 1)]
-        for e in engs[1:]:
-            assert e.set_message(LIB_MESSAGE) == 0
-        streams = [torch.cuda.Stream(dev) for _ in engs]
-        codes_p = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in engs]
-
-        def pstep():
-            for e, st, cd in zip(engs, streams, codes_p):
-                e.verify_batch_device(d_pks.data_ptr(), d_sigs.data_ptr(), n, cd.data_ptr(), st.cuda_stream)
-
-        for _ in range(args.warmup):
-            pstep()
-        torch.cuda.synchronize(dev)
-        for cd in codes_p:
-            assert np.array_equal(cd.cpu().numpy(), expect), "pipelined verdicts differ"
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            pstep()
-        torch.cuda.synchronize(dev)
-        if dist:
-            tdist.barrier()
-        pdt = time.perf_counter() - t0
-        if dist:
-            t = torch.tensor([pdt], dtype=torch.float64, device=coll_dev)
-            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-            pdt = float(t.item())
-        for cd in codes_p:
-            assert np.array_equal(cd.cpu().numpy(), expect)
-        pipelined = {"value": round(n * len(engs) * args.steps * world / pdt, 1), "unit": "verifications/s",
-                     "batches_in_flight": len(engs), "batch": n,
-                     "ms_per_step": round(pdt / args.steps * 1e3, 4),
-                     "note": "same batch of 4096 on each of the streams; throughput with batches overlapped"}
-        for e in engs[1:]:
-            e.close()
+            pdt = timer.run(pstep, args.steps, args.warmup)
+            for cd in codes_p:
+                head.check(cd)
+            extra["pipelined"] = {"value": round(n * len(engs) * args.steps * world / pdt, 1),
+                                  "unit": "verifications/s", "batches_in_flight": len(engs), "batch": n,
+                                  "ms_per_step": round(pdt / args.steps * 1e3, 4),
+                                  "note": "headline batch on each of the streams; throughput with batches overlapped"}
+            for e in engs[1:]:
+                e.close()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            cpu = cpu_baseline(min(n, 4096), pks, sigs, expect)
+            cpu = cpu_baseline_aggregate(head.reg, head.reqs, head.words, head.sigs, head.expect, args.cpu_sample)
         except Exception as e:  # pragma: no cover - reported, not fatal
             cpu = {"error": str(e)}
     if rank == 0:
+        workload = (f"config 5: one committee of {n_reg} signers per GPU, {n} multisigs at random Handel levels"
+                    if args.committees else
+                    f"config 3: {n} Handel multisigs per GPU on a {n_reg}-key registry, random node/level")
         line = {
             "metric": "BN254 aggregate-sig verifications/sec (batch 4096)",
             "value": round(value, 1),
@@ -367,14 +498,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32 (26-bit-limb Fp, 64-bit accumulators)",
-            "data": "synthetic (seeded keys, lib.Message, 1/8 tampered signatures)",
-            "config": {"workload": "config 2: 4096 independent BLS pairing checks per GPU (bn256, dclxvi curve)",
-                       "batch_per_gpu": n, "message": "lib.Message (81 B)", "parallelism": f"dp{world} (replicated registry, sharded batches)"},
-            "roofline": roofline,
+            "data": "synthetic (seeded keys, lib.Message, bitset density U[0.5,1], 1/8 tampered aggregates)",
+            "config": {"workload": workload + ", bitset density U[0.5,1], 1/8 tampered",
+                       "batch_per_gpu": n, "registry": n_reg, "message": "lib.Message (81 B)",
+                       "signers_per_check_mean": round(float(head.signers.mean()), 1),
+                       "signers_per_check_max": int(head.signers.max()),
+                       "parallelism": f"dp{world} (one batch per GPU, RCCL all_gather of verdict bitsets)"},
+            "roofline": roof,
+            "roofline_k_verify": roof_verify,
             "cpu_baseline": cpu,
-            "aggregate": aggregate,
-            "aggregate_full_registry": aggregate_full,
-            "pipelined": pipelined,
+            **extra,
         }
         print(json.dumps(line))
     eng.close()

@@ -26,11 +26,19 @@ HG_ERR_EMPTY_AGG = 6
 HG_ERR_CF_EXCEEDS = 7
 HG_ERR_CF_MALFORMED = 8
 HG_ERR_CF_SHORT = 9
+HG_ERR_SIG_CF_EXCEEDS = 10
+HG_ERR_SIG_CF_MALFORMED = 11
+HG_ERR_SIG_CF_SHORT = 12
+HG_ERR_MULTI_SIZES = 13
 HG_ERR_ARG = 100
 HG_ERR_DEVICE = 101
 
 HG_FLAVOR_GO = 0
 HG_FLAVOR_CF = 1
+
+HG_PHASE_VERIFY = 0
+HG_PHASE_AGGREGATE = 1
+HG_PHASE_SUBMIT = 2
 
 # every symbol include/handel_gpu.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
@@ -42,25 +50,31 @@ SIGNATURES = {
     "hg_destroy": (None, [_P]),
     "hg_last_error": (ctypes.c_char_p, [_P]),
     "hg_code_string": (ctypes.c_char_p, [_I, _I]),
+    "hg_processing_error_string": (ctypes.c_char_p, [_I, _I]),
     "hg_registry_load": (_I, [_P, _P, _SZ, _P]),
     "hg_registry_size": (_SZ, [_P]),
     "hg_set_message": (_I, [_P, _P, _SZ]),
     "hg_verify_batch": (_I, [_P, _P, _P, _SZ, _P]),
+    "hg_verify_batch_msg": (_I, [_P, _P, _SZ, _P, _P, _SZ, _P]),
     "hg_verify_batch_device": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "hg_pack_verdicts_device": (_I, [_P, _P, _SZ, _P, _P]),
     "hg_verify_aggregate": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P, _P]),
     "hg_verify_aggregate_device": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
+    "hg_verify_aggregate_msg": (_I, [_P, _P, _SZ, _P, _SZ, _P, _SZ, _P, _P, _P]),
+    "hg_verify_multisig": (_I, [_P, _P, _P, _SZ, _P, _SZ, _P, _P]),
     "hg_aggregate_pk": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P]),
     "hg_combine_g1": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "hg_combine_g2": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "hg_pair": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "hg_keygen": (_I, [_P, _P, _SZ, _P]),
     "hg_sign": (_I, [_P, _P, _SZ, _P]),
+    "hg_sign_msg": (_I, [_P, _P, _SZ, _P, _SZ, _P]),
     "hg_debug_fp_mul": (_I, [_P, _P, _P, _SZ, _P]),
     "hg_diag_read": (_I, [_P, _P, _SZ]),
     "hg_debug_fp12": (_I, [_P, _I, _P, _P, _SZ, _P]),
     "hg_timing_enable": (_I, [_P, _I]),
     "hg_timing_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
+    "hg_timing_read_phase": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
     "hg_sync": (_I, [_P]),
 }
 

@@ -14,7 +14,7 @@ import os
 import threading
 from typing import Optional
 
-from ._lib import HG_ERR_HASH_EOF, HG_OK
+from ._lib import HG_ERR_HASH_EOF, HG_OK, HandelGPUError
 from .engine import Engine
 
 ORDER = 65000549695646603732796438742359905742570406053903786389881062969044166799969
@@ -72,7 +72,9 @@ class PublicKey(_Base):
         out, codes = e.combine_g2(bytes(buff[:128]), bytes(128))
         if codes[0] != HG_OK:
             raise BN256Error(e.code_string(int(codes[0])))
-        self.p = bytes(buff[:128])
+        # keep the GPU's re-encoding of the decoded point: x/crypto takes
+        # coordinates mod p and its Marshal writes them reduced
+        self.p = out
 
     def Combine(self, other: "PublicKey") -> "PublicKey":
         """bn256/go/bn256.go:97-105: nil receiver returns the argument."""
@@ -88,9 +90,9 @@ class PublicKey(_Base):
         e = self._eng()
         if self.p is None:
             raise BN256Error("runtime error: invalid memory address or nil pointer dereference")
-        if e.set_message(msg) == HG_ERR_HASH_EOF:
-            return BN256Error("EOF")
-        codes = e.verify_batch(self.p, sig.MarshalBinary())
+        # hashing and the check under one lock hold of the shared context, so
+        # concurrent callers with different messages cannot interleave
+        codes = e.verify_batch_msg(msg, self.p, sig.MarshalBinary())
         if codes[0] == HG_OK:
             return None
         return BN256Error(e.code_string(int(codes[0])))
@@ -115,11 +117,9 @@ class SigBLS(_Base):
             raise BN256Error("bn256: multisig can't unmarshal: bn256: not enough data")
         out, codes = e.combine_g1(bytes(b[:64]), bytes(64))
         if codes[0] != HG_OK:
-            text = e.code_string(int(codes[0]))
-            if self.flavor == "go":
-                raise BN256Error("bn256: multisig can't unmarshal")
-            raise BN256Error(text if text.startswith("bn256: multisig") else "bn256: multisig can't unmarshal: " + text)
-        self.e = bytes(b[:64])
+            # go: "bn256: multisig can't unmarshal"; cf: the G1 error wrapped (bn256/cf/bn256.go:183-190)
+            raise BN256Error(e.code_string(int(codes[0])))
+        self.e = out  # re-encoded (reduced) like the upstream Marshal
 
     def Combine(self, other: "SigBLS") -> "SigBLS":
         if self.e is None:
@@ -138,9 +138,12 @@ class SecretKey(_Base):
 
     def Sign(self, msg: bytes, reader=None) -> SigBLS:
         e = self._eng()
-        if e.set_message(msg) == HG_ERR_HASH_EOF:
-            raise BN256Error("EOF")
-        return SigBLS(e.sign(self.s.to_bytes(32, "big")))
+        try:
+            return _flavored(SigBLS, self.flavor)(e.sign_msg(msg, self.s.to_bytes(32, "big")))
+        except HandelGPUError as err:
+            if f"code {HG_ERR_HASH_EOF}:" in str(err):
+                raise BN256Error("EOF") from None
+            raise
 
     def MarshalBinary(self) -> bytes:
         return self.s.to_bytes((self.s.bit_length() + 7) // 8, "big")
@@ -168,15 +171,28 @@ def NewKeyPair(reader=None):
     return SecretKey(k), PublicKey(pk)
 
 
+_classes = {}
+
+
+def _flavored(base, flavor: str):
+    """The subclass of base bound to one upstream flavor (one per (base, flavor))."""
+    if base.flavor == flavor:
+        return base
+    with _eng_lock:
+        key = (base, flavor)
+        if key not in _classes:
+            _classes[key] = type(base.__name__, (base,), {"flavor": flavor})
+        return _classes[key]
+
+
 class Constructor:
     """bn256/go/bn256.go:34-67 / cf: the handel.Constructor + simul extension."""
 
     def __init__(self, flavor: str = "go"):
         self.flavor = flavor
-        ns = {"flavor": flavor}
-        self._pk = type("PublicKey", (PublicKey,), ns)
-        self._sig = type("SigBLS", (SigBLS,), ns)
-        self._sk = type("SecretKey", (SecretKey,), ns)
+        self._pk = _flavored(PublicKey, flavor)
+        self._sig = _flavored(SigBLS, flavor)
+        self._sk = _flavored(SecretKey, flavor)
 
     def Signature(self) -> SigBLS:
         return self._sig()

@@ -68,5 +68,27 @@ def build_library(force: bool = False, verbose: bool = True, diag: bool = False)
     return lib
 
 
+ABI_THREADS = os.path.join(OUT_DIR, "abi_threads")
+
+
+def build_native_tests(verbose: bool = True) -> str:
+    """tests/native/abi_threads.c (the C-level thread-safety test of the ABI),
+    linked against the in-tree library only through include/handel_gpu.h. A
+    test harness, not product code: built here so the GPU box runs it as is."""
+    src = os.path.join(HERE, "..", "tests", "native", "abi_threads.c")
+    if os.path.exists(ABI_THREADS) and os.path.getmtime(ABI_THREADS) >= max(os.path.getmtime(src),
+                                                                           os.path.getmtime(LIB)):
+        return ABI_THREADS
+    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-I", os.path.join(HERE, "..", "include"), src,
+           "-L", OUT_DIR, "-lhandel_gpu", "-lpthread", "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib",
+           "-Wl,-rpath,$ORIGIN", "-o", ABI_THREADS]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return ABI_THREADS
+
+
 if __name__ == "__main__":
     print(build_library(force="--force" in sys.argv, diag="--diag" in sys.argv))
+    if "--diag" not in sys.argv:
+        print(build_native_tests())

@@ -61,10 +61,12 @@ HG_DEV int32_t decode_g1_one(const uint8_t* m, int flavor, PointG1& P) {
   for (int k = 0; k < 64; k++) nz |= m[k] != 0;
   int32_t code = HG_OK;
   P.inf = nz ? 0u : 1u;
+  // every G1 point this API decodes is a signature: cloudflare's
+  // SigBLS.UnmarshalBinary wraps the G1 error (bn256/cf/bn256.go:183-190)
   if (flavor == HG_FLAVOR_CF && (gx || gy)) {
-    code = HG_ERR_CF_EXCEEDS;
+    code = HG_ERR_SIG_CF_EXCEEDS;
   } else if (nz && !g1_on_curve(P.x, P.y)) {
-    code = flavor == HG_FLAVOR_CF ? HG_ERR_CF_MALFORMED : HG_ERR_SIG_UNMARSHAL;
+    code = flavor == HG_FLAVOR_CF ? HG_ERR_SIG_CF_MALFORMED : HG_ERR_SIG_UNMARSHAL;
   }
   return code;
 }

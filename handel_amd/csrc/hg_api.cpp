@@ -153,7 +153,8 @@ struct hg_ctx {
   uint32_t* d_k = nullptr;
   bool has_msg = false;
   bool hash_eof = false;
-  // registry
+  std::vector<uint8_t> msg;  // the message d_h was hashed from (hg_*_msg cache)
+  // registry (nreg > 0 only while every table below matches it)
   DevBuf<PointG2> reg;
   size_t nreg = 0;
   // aligned block sums of the registry (level k block j at blocks[block_base[k] + j])
@@ -169,24 +170,67 @@ struct hg_ctx {
   DevBuf<CheckIn> checks;
   DevBuf<int32_t> codes_a, codes_b, codes_c;
   DevBuf<hg_request> reqs;
-  DevBuf<int> order;  // aggregation schedule (k_agg_order)
+  DevBuf<int> order;       // aggregation schedule (k_agg_order)
   DevBuf<uint8_t> agg_ws;  // per-request fold results (k_aggregate -> k_agg_finish)
   DevBuf<uint64_t> words;
-  // optional per-launch timing of the pairing-check kernel (bench roofline)
+  // submission order across streams: the event recorded after the last
+  // submission and the stream it ran on (the workspaces above are shared)
+  hipEvent_t last_ev = nullptr;
+  hipStream_t last_s = nullptr;
+  // optional per-phase timing (bench roofline), see hg_timing_read_phase
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> verify_events;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events[HG_NUM_PHASES];
+};
+
+// ---------------------------------------------------------------- submission order
+// Every device submission of a context runs between begin() and end(): a
+// submission on another stream than the previous one first waits for the
+// previous one's event, so two submissions never use the shared workspaces
+// (or the registry tables and H) at the same time.
+static hipError_t begin(hg_ctx* c, hipStream_t s) {
+  if (c->last_ev && c->last_s != s) return hipStreamWaitEvent(s, c->last_ev, 0);
+  return hipSuccess;
+}
+static hipError_t end(hg_ctx* c, hipStream_t s) {
+  if (!c->last_ev) {
+    hipError_t e = hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  c->last_s = s;
+  return hipEventRecord(c->last_ev, s);
+}
+
+// ---------------------------------------------------------------- timing
+struct PhaseTimer {
+  hg_ctx* c;
+  int phase;
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  PhaseTimer(hg_ctx* c_, int phase_, hipStream_t s_) : c(c_), phase(phase_), s(s_) {
+    if (!c->timing) return;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+      if (a) (void)hipEventDestroy(a);
+      a = b = nullptr;
+      return;
+    }
+    (void)hipEventRecord(a, s);
+  }
+  void stop() {
+    if (!a) return;
+    (void)hipEventRecord(b, s);
+    c->events[phase].emplace_back(a, b);
+    a = b = nullptr;
+  }
+  ~PhaseTimer() {  // an error path that never reached stop(): discard
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+  }
 };
 
 static void timed_verify(hg_ctx* c, const CheckIn* in, int n, int32_t* codes, hipStream_t s) {
-  hipEvent_t a = nullptr, b = nullptr;
-  if (c->timing && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) {
-    (void)hipEventRecord(a, s);
-    launch_verify(in, n, c->d_lines, c->d_h, codes, s);
-    (void)hipEventRecord(b, s);
-    c->verify_events.emplace_back(a, b);
-    return;
-  }
+  PhaseTimer t(c, HG_PHASE_VERIFY, s);
   launch_verify(in, n, c->d_lines, c->d_h, codes, s);
+  t.stop();
 }
 
 #define HG_CHECK(ctx, expr)                                                        \
@@ -209,9 +253,229 @@ static int check_launch(hg_ctx* c) {
   return HG_OK;
 }
 
+static void release_all(hg_ctx* c) {
+  c->reg.release();
+  c->blocks.release();
+  c->wsum.release();
+  c->bytes_a.release();
+  c->bytes_b.release();
+  c->pts2.release();
+  c->pts1.release();
+  c->pts1b.release();
+  c->checks.release();
+  c->codes_a.release();
+  c->codes_b.release();
+  c->codes_c.release();
+  c->reqs.release();
+  c->order.release();
+  c->agg_ws.release();
+  c->words.release();
+  for (auto& ph : c->events) {
+    for (auto& pr : ph) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    ph.clear();
+  }
+  if (c->last_ev) (void)hipEventDestroy(c->last_ev);
+  c->last_ev = nullptr;
+  if (c->d_lines) (void)hipFree(c->d_lines);
+  if (c->d_h) (void)hipFree(c->d_h);
+  if (c->d_k) (void)hipFree(c->d_k);
+  c->d_lines = nullptr;
+  c->d_h = nullptr;
+  c->d_k = nullptr;
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  c->stream = nullptr;
+}
+
+// hashedMessage into d_h (the caller holds the lock); HG_OK or HG_ERR_HASH_EOF
+static int set_message_locked(hg_ctx* c, const uint8_t* msg, size_t len) {
+  HG_CHECK(c, hipSetDevice(c->device));
+  if (c->has_msg && c->msg.size() == len && (len == 0 || memcmp(c->msg.data(), msg, len) == 0))
+    return c->hash_eof ? HG_ERR_HASH_EOF : HG_OK;
+  uint8_t d[32];
+  sha256(msg, len, d);
+  uint32_t k[8];
+  c->has_msg = false;
+  c->msg.assign(msg, msg + len);
+  c->hash_eof = !hash_scalar(d, k);
+  if (c->hash_eof) {
+    c->has_msg = true;
+    return HG_ERR_HASH_EOF;
+  }
+  HG_CHECK(c, begin(c, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->d_k, k, sizeof k, hipMemcpyHostToDevice, c->stream));
+  launch_hash_point(c->d_k, c->d_h, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  c->has_msg = true;
+  return HG_OK;
+}
+
+static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n,
+                                      int32_t* d_codes, hipStream_t s) {
+  if (!c->has_msg) {
+    c->err = "hg_set_message was not called";
+    return HG_ERR_ARG;
+  }
+  HG_CHECK(c, c->checks.ensure(n));
+  HG_CHECK(c, begin(c, s));
+  PhaseTimer all(c, HG_PHASE_SUBMIT, s);
+  launch_decode_checks(d_pks, d_sigs, (int)n, c->flavor, c->checks.p, d_codes, s);
+  if (c->hash_eof) k_fill_codes<<<nb(n), 256, 0, s>>>(d_codes, (int)n, HG_OK, HG_ERR_HASH_EOF);
+  else timed_verify(c, c->checks.p, (int)n, d_codes, s);
+  all.stop();
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, end(c, s));
+  return HG_OK;
+}
+
+static int verify_batch_host_locked(hg_ctx* c, const uint8_t* pks, const uint8_t* sigs, size_t n, int32_t* codes) {
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 128));
+  HG_CHECK(c, c->bytes_b.ensure(n * 64));
+  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, begin(c, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, pks, n * 128, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
+  int rc = verify_batch_device_locked(c, c->bytes_a.p, c->bytes_b.p, n, c->codes_c.p, c->stream);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+// host-side request validation: the level check of processing.go:350-352
+static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector<int32_t>& out) {
+  out.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    const hg_request& r = reqs[i];
+    bool ok = r.bitlen == r.level_size && (size_t)r.offset + r.bitlen <= c->nreg;
+    out[i] = ok ? HG_OK : HG_ERR_LEVEL;
+  }
+}
+
+// The Combine fold and (verify) the pairing check of n requests, device
+// pointers, on stream s; d_lvl holds the level codes and is updated in place.
+static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                                   const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
+                                   bool verify, hipStream_t s) {
+  if (verify && !c->has_msg) {
+    c->err = "hg_set_message was not called";
+    return HG_ERR_ARG;
+  }
+  HG_CHECK(c, c->checks.ensure(n));
+  HG_CHECK(c, c->order.ensure(n));
+  HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
+  if (d_agg) HG_CHECK(c, c->pts2.ensure(n));
+  if (verify) {
+    HG_CHECK(c, c->pts1.ensure(n));
+    HG_CHECK(c, c->codes_b.ensure(n));
+  }
+  HG_CHECK(c, begin(c, s));
+  PhaseTimer all(c, HG_PHASE_SUBMIT, s);
+  PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
+  launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
+                   d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
+  fold.stop();
+  if (d_agg) {
+    launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);
+    launch_encode_g2(c->pts2.p, (int)n, d_agg, s);
+  }
+  if (verify) {
+    launch_decode_g1(d_sigs, (int)n, c->flavor, c->pts1.p, c->codes_b.p, s);
+    k_agg_codes<<<nb(n), 256, 0, s>>>(c->codes_b.p, d_lvl, c->hash_eof ? 1 : 0, (int)n, d_codes);
+    if (!c->hash_eof) {
+      launch_sig_into_checks(c->pts1.p, (int)n, c->checks.p, s);
+      timed_verify(c, c->checks.p, (int)n, d_codes, s);
+    }
+  }
+  all.stop();
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, end(c, s));
+  return HG_OK;
+}
+
+__global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool ok = r[i].bitlen == r[i].level_size && (uint64_t)r[i].offset + r[i].bitlen <= nreg;
+  out[i] = ok ? HG_OK : HG_ERR_LEVEL;
+}
+
+static int aggregate_host_locked(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
+                                 const uint8_t* sigs, int32_t* codes, uint8_t* agg_out, bool verify) {
+  HG_CHECK(c, hipSetDevice(c->device));
+  std::vector<int32_t> lvl;
+  level_codes(c, reqs, n, lvl);
+  for (size_t i = 0; i < n; i++) {
+    if (lvl[i] == HG_OK && (size_t)reqs[i].word_offset + (reqs[i].bitlen + 63) / 64 > nwords) {
+      c->err = "request words out of range";
+      return HG_ERR_ARG;
+    }
+  }
+  HG_CHECK(c, c->reqs.ensure(n));
+  HG_CHECK(c, c->words.ensure(nwords ? nwords : 1));
+  HG_CHECK(c, c->codes_a.ensure(n));
+  HG_CHECK(c, c->codes_c.ensure(n));
+  uint8_t* d_agg = nullptr;
+  if (agg_out) {
+    HG_CHECK(c, c->bytes_a.ensure(n * 128));
+    d_agg = c->bytes_a.p;
+  }
+  if (verify) HG_CHECK(c, c->bytes_b.ensure(n * 64));
+  HG_CHECK(c, begin(c, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->reqs.p, reqs, n * sizeof(hg_request), hipMemcpyHostToDevice, c->stream));
+  if (nwords) HG_CHECK(c, hipMemcpyAsync(c->words.p, words, nwords * 8, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->codes_c.p, lvl.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  if (verify) HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
+  int rc = aggregate_device_locked(c, c->reqs.p, n, c->words.p, verify ? c->bytes_b.p : nullptr, c->codes_a.p, d_agg,
+                                   c->codes_c.p, verify, c->stream);
+  if (rc) return rc;
+  if (agg_out) HG_CHECK(c, hipMemcpyAsync(agg_out, d_agg, n * 128, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, verify ? c->codes_a.p : c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  if (agg_out) {
+    // the reference has no aggregate for level errors / empty bitsets: zero them
+    for (size_t i = 0; i < n; i++)
+      if (lvl[i] != HG_OK || codes[i] == HG_ERR_EMPTY_AGG) memset(agg_out + 128 * i, 0, 128);
+  }
+  return HG_OK;
+}
+
+static int sign_locked(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out) {
+  if (!c->has_msg) {
+    c->err = "hg_set_message was not called";
+    return HG_ERR_ARG;
+  }
+  if (c->hash_eof) return HG_ERR_HASH_EOF;
+  if (n == 0) return HG_OK;
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, c->bytes_a.ensure(n * 64));
+  HG_CHECK(c, c->bytes_b.ensure(n * 32));
+  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, begin(c, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
+  launch_g1_mul(c->d_h, c->bytes_b.p, (int)n, c->pts1.p, c->stream);
+  launch_encode_g1(c->pts1.p, (int)n, c->bytes_a.p, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(sigs_out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
 extern "C" {
 
-int hg_version(void) { return 1; }
+int hg_version(void) { return 2; }
 
 const char* hg_code_string(int code, int flavor) {
   switch (code) {
@@ -226,8 +490,21 @@ const char* hg_code_string(int code, int flavor) {
     case HG_ERR_CF_EXCEEDS: return "bn256: coordinate exceeds modulus";
     case HG_ERR_CF_MALFORMED: return "bn256: malformed point";
     case HG_ERR_CF_SHORT: return "bn256: not enough data";
+    case HG_ERR_SIG_CF_EXCEEDS: return "bn256: multisig can't unmarshal: bn256: coordinate exceeds modulus";
+    case HG_ERR_SIG_CF_MALFORMED: return "bn256: multisig can't unmarshal: bn256: malformed point";
+    case HG_ERR_SIG_CF_SHORT: return "bn256: multisig can't unmarshal: bn256: not enough data";
+    case HG_ERR_MULTI_SIZES: return "verify multisignature: inconsistent sizes";
     case HG_ERR_ARG: return "invalid argument";
     default: return "device error";
+  }
+}
+
+const char* hg_processing_error_string(int code, int flavor) {
+  // processing.go:361-365 wraps only VerifySignature's error: fmt.Errorf("handel: %s", err)
+  switch (code) {
+    case HG_ERR_SIG_INVALID: return "handel: bn256: signature invalid";
+    case HG_ERR_HASH_EOF: return "handel: EOF";
+    default: return hg_code_string(code, flavor);
   }
 }
 
@@ -246,12 +523,14 @@ int hg_create(int device, int flavor, hg_ctx** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_k, sizeof(uint32_t) * 8);
   if (e != hipSuccess) {
     fprintf(stderr, "hg_create: %s\n", hipGetErrorString(e));
+    release_all(c);
     delete c;
     return HG_ERR_DEVICE;
   }
   launch_g2_lines(c->d_lines, c->stream);
   if (check_launch(c) != HG_OK || hipStreamSynchronize(c->stream) != hipSuccess) {
     fprintf(stderr, "hg_create: %s\n", c->err.c_str());
+    release_all(c);
     delete c;
     return HG_ERR_DEVICE;
   }
@@ -263,53 +542,36 @@ void hg_destroy(hg_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  c->reg.release();
-  c->bytes_a.release();
-  c->bytes_b.release();
-  c->pts2.release();
-  c->pts1.release();
-  c->pts1b.release();
-  c->checks.release();
-  c->codes_a.release();
-  c->codes_b.release();
-  c->codes_c.release();
-  c->reqs.release();
-  c->words.release();
-  if (c->d_lines) (void)hipFree(c->d_lines);
-  if (c->d_h) (void)hipFree(c->d_h);
-  if (c->d_k) (void)hipFree(c->d_k);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->last_ev) (void)hipEventSynchronize(c->last_ev);  // a submission on a caller stream
+  release_all(c);
   delete c;
 }
 
 int hg_sync(hg_ctx* c) {
   if (!c) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
+  if (c->last_ev) HG_CHECK(c, hipEventSynchronize(c->last_ev));
   return HG_OK;
 }
 
 int hg_set_message(hg_ctx* c, const uint8_t* msg, size_t len) {
   if (!c || (!msg && len)) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  HG_CHECK(c, hipSetDevice(c->device));
-  uint8_t d[32];
-  sha256(msg, len, d);
-  uint32_t k[8];
-  c->has_msg = true;
-  c->hash_eof = !hash_scalar(d, k);
-  if (c->hash_eof) return HG_ERR_HASH_EOF;
-  HG_CHECK(c, hipMemcpyAsync(c->d_k, k, sizeof k, hipMemcpyHostToDevice, c->stream));
-  launch_hash_point(c->d_k, c->d_h, c->stream);
-  int rc = check_launch(c);
-  if (rc) return rc;
-  HG_CHECK(c, hipStreamSynchronize(c->stream));
-  return HG_OK;
+  return set_message_locked(c, msg, len);
 }
 
 int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   if (!c || (!pks && n)) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
+  // until every table is rebuilt the context has no registry: a failure below
+  // leaves it empty (every aggregate request then fails its range check)
+  c->nreg = 0;
+  c->block_levels = 0;
+  HG_CHECK(c, begin(c, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
   HG_CHECK(c, c->reg.ensure(n));
   HG_CHECK(c, c->bytes_a.ensure(n * 128));
   HG_CHECK(c, c->codes_a.ensure(n));
@@ -323,8 +585,6 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   int bad = 0;
   for (size_t i = 0; i < n; i++) bad |= h[i] != HG_OK;
   if (codes && n) memcpy(codes, h.data(), n * 4);
-  c->nreg = n;
-  c->block_levels = 0;
   if (bad) {
     c->err = "registry contains keys that fail to unmarshal";
     return HG_ERR_PK_UNMARSHAL;
@@ -332,23 +592,22 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   // sums of the aligned power-of-two blocks (Handel's level ranges), level by level
   int K = 0;
   while (K < 23 && ((size_t)1 << K) < n) K++;
-  std::vector<size_t> nb(K + 1, 0);
-  nb[0] = n;
+  std::vector<size_t> nbk(K + 1, 0);
+  nbk[0] = n;
   size_t total = 0;
   for (int k = 1; k <= K; k++) {
-    nb[k] = (n + ((size_t)1 << k) - 1) >> k;
+    nbk[k] = (n + ((size_t)1 << k) - 1) >> k;
     c->block_base[k] = (int)total;
-    total += nb[k];
+    total += nbk[k];
   }
   if (total) {
     HG_CHECK(c, c->blocks.ensure(total));
     for (int k = 1; k <= K; k++) {
       const PointG2* src = k == 1 ? c->reg.p : c->blocks.p + c->block_base[k - 1];
-      launch_block_sums(src, (int)nb[k - 1], c->blocks.p + c->block_base[k], (int)nb[k], c->stream);
+      launch_block_sums(src, (int)nbk[k - 1], c->blocks.p + c->block_base[k], (int)nbk[k], c->stream);
     }
     rc = check_launch(c);
     if (rc) return rc;
-    HG_CHECK(c, hipStreamSynchronize(c->stream));
   }
   const size_t nwin = (n + 7) / 8;
   if (nwin) {
@@ -356,33 +615,23 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
     launch_window_sums(c->reg.p, (int)n, c->wsum.p, (int)nwin, c->stream);
     rc = check_launch(c);
     if (rc) return rc;
-    HG_CHECK(c, hipStreamSynchronize(c->stream));
   }
+  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
   c->block_levels = K;
+  c->nreg = n;
   return HG_OK;
 }
 
-size_t hg_registry_size(hg_ctx* c) { return c ? c->nreg : 0; }
-
-static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n,
-                                      int32_t* d_codes, hipStream_t s) {
-  if (!c->has_msg) {
-    c->err = "hg_set_message was not called";
-    return HG_ERR_ARG;
-  }
-  HG_CHECK(c, c->checks.ensure(n));
-  launch_decode_checks(d_pks, d_sigs, (int)n, c->flavor, c->checks.p, d_codes, s);
-  if (c->hash_eof) {
-    k_fill_codes<<<nb(n), 256, 0, s>>>(d_codes, (int)n, HG_OK, HG_ERR_HASH_EOF);
-    return check_launch(c);
-  }
-  timed_verify(c, c->checks.p, (int)n, d_codes, s);
-  return check_launch(c);
+size_t hg_registry_size(hg_ctx* c) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  return c->nreg;
 }
 
 int hg_verify_batch_device(hg_ctx* c, const uint8_t* d_pks, const uint8_t* d_sigs, size_t n, int32_t* d_codes,
                            void* stream) {
-  if (!c || (n && (!d_pks || !d_sigs || !d_codes))) return HG_ERR_ARG;
+  if (!c || (n && (!d_pks || !d_sigs || !d_codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
@@ -395,147 +644,90 @@ int hg_pack_verdicts_device(hg_ctx* c, const int32_t* d_codes, size_t n, uint8_t
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
-  launch_pack_verdicts(d_codes, (int)n, d_bits, stream ? (hipStream_t)stream : c->stream);
-  return check_launch(c);
-}
-
-int hg_verify_batch(hg_ctx* c, const uint8_t* pks, const uint8_t* sigs, size_t n, int32_t* codes) {
-  if (!c || (n && (!pks || !sigs || !codes))) return HG_ERR_ARG;
-  if (n == 0) return HG_OK;
-  std::lock_guard<std::mutex> g(c->mu);
-  HG_CHECK(c, hipSetDevice(c->device));
-  HG_CHECK(c, c->bytes_a.ensure(n * 128));
-  HG_CHECK(c, c->bytes_b.ensure(n * 64));
-  HG_CHECK(c, c->codes_c.ensure(n));
-  HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, pks, n * 128, hipMemcpyHostToDevice, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
-  int rc = verify_batch_device_locked(c, c->bytes_a.p, c->bytes_b.p, n, c->codes_c.p, c->stream);
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  HG_CHECK(c, begin(c, s));
+  launch_pack_verdicts(d_codes, (int)n, d_bits, s);
+  int rc = check_launch(c);
   if (rc) return rc;
-  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  HG_CHECK(c, end(c, s));
   return HG_OK;
 }
 
-// host-side request validation: the level check of processing.go:350-352
-static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector<int32_t>& out, bool* range_ok) {
-  out.resize(n);
-  *range_ok = true;
-  for (size_t i = 0; i < n; i++) {
-    const hg_request& r = reqs[i];
-    bool ok = r.bitlen == r.level_size && (size_t)r.offset + r.bitlen <= c->nreg;
-    out[i] = ok ? HG_OK : HG_ERR_LEVEL;
-  }
+int hg_verify_batch(hg_ctx* c, const uint8_t* pks, const uint8_t* sigs, size_t n, int32_t* codes) {
+  if (!c || (n && (!pks || !sigs || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  return verify_batch_host_locked(c, pks, sigs, n, codes);
 }
 
-static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
-                                   const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
-                                   bool verify, hipStream_t s) {
-  HG_CHECK(c, c->checks.ensure(n));
-  HG_CHECK(c, c->order.ensure(n));
-  HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
-  launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
-                   d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
-  if (d_agg) {
-    HG_CHECK(c, c->pts2.ensure(n));
-    launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);
-    launch_encode_g2(c->pts2.p, (int)n, d_agg, s);
-  }
-  if (!verify) return check_launch(c);
-  if (!c->has_msg) {
-    c->err = "hg_set_message was not called";
-    return HG_ERR_ARG;
-  }
-  HG_CHECK(c, c->pts1.ensure(n));
-  HG_CHECK(c, c->codes_b.ensure(n));
-  launch_decode_g1(d_sigs, (int)n, c->flavor, c->pts1.p, c->codes_b.p, s);
-  k_agg_codes<<<nb(n), 256, 0, s>>>(c->codes_b.p, d_lvl, c->hash_eof ? 1 : 0, (int)n, d_codes);
-  if (!c->hash_eof) {
-    launch_sig_into_checks(c->pts1.p, (int)n, c->checks.p, s);
-    timed_verify(c, c->checks.p, (int)n, d_codes, s);
-  }
-  return check_launch(c);
-}
-
-__global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t* out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  bool ok = r[i].bitlen == r[i].level_size && (uint64_t)r[i].offset + r[i].bitlen <= nreg;
-  out[i] = ok ? HG_OK : HG_ERR_LEVEL;
+int hg_verify_batch_msg(hg_ctx* c, const uint8_t* msg, size_t len, const uint8_t* pks, const uint8_t* sigs, size_t n,
+                        int32_t* codes) {
+  if (!c || (!msg && len) || (n && (!pks || !sigs || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  int rc = set_message_locked(c, msg, len);
+  if (rc != HG_OK && rc != HG_ERR_HASH_EOF) return rc;
+  if (n == 0) return HG_OK;
+  return verify_batch_host_locked(c, pks, sigs, n, codes);
 }
 
 int hg_verify_aggregate_device(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
                                const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg_pk_out, void* stream) {
-  if (!c || (n && (!d_reqs || !d_sigs || !d_codes))) return HG_ERR_ARG;
+  if (!c || (n && (!d_reqs || !d_sigs || !d_codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, begin(c, s));
   k_level_codes<<<nb(n), 256, 0, s>>>(d_reqs, (int)n, (uint32_t)c->nreg, c->codes_c.p);
   return aggregate_device_locked(c, d_reqs, n, d_words, d_sigs, d_codes, d_agg_pk_out, c->codes_c.p, true, s);
 }
 
-static int aggregate_host(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
-                          const uint8_t* sigs, int32_t* codes, uint8_t* agg_out, bool verify) {
-  std::vector<int32_t> lvl;
-  bool range_ok;
-  level_codes(c, reqs, n, lvl, &range_ok);
-  for (size_t i = 0; i < n; i++) {
-    if (lvl[i] == HG_OK && (size_t)reqs[i].word_offset + (reqs[i].bitlen + 63) / 64 > nwords) {
-      c->err = "request words out of range";
-      return HG_ERR_ARG;
-    }
-  }
-  HG_CHECK(c, c->reqs.ensure(n));
-  HG_CHECK(c, c->words.ensure(nwords ? nwords : 1));
-  HG_CHECK(c, c->codes_a.ensure(n));
-  HG_CHECK(c, c->codes_c.ensure(n));
-  HG_CHECK(c, hipMemcpyAsync(c->reqs.p, reqs, n * sizeof(hg_request), hipMemcpyHostToDevice, c->stream));
-  if (nwords) HG_CHECK(c, hipMemcpyAsync(c->words.p, words, nwords * 8, hipMemcpyHostToDevice, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(c->codes_c.p, lvl.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-  uint8_t* d_agg = nullptr;
-  if (agg_out) {
-    HG_CHECK(c, c->bytes_a.ensure(n * 128));
-    d_agg = c->bytes_a.p;
-  }
-  if (verify) {
-    HG_CHECK(c, c->bytes_b.ensure(n * 64));
-    HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
-  }
-  int rc = aggregate_device_locked(c, c->reqs.p, n, c->words.p, verify ? c->bytes_b.p : nullptr, c->codes_a.p, d_agg,
-                                   c->codes_c.p, verify, c->stream);
-  if (rc) return rc;
-  if (agg_out) HG_CHECK(c, hipMemcpyAsync(agg_out, d_agg, n * 128, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(codes, verify ? c->codes_a.p : c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipStreamSynchronize(c->stream));
-  if (agg_out) {
-    // the reference has no aggregate for level errors / empty bitsets: zero them
-    for (size_t i = 0; i < n; i++)
-      if (lvl[i] != HG_OK || codes[i] == HG_ERR_EMPTY_AGG) memset(agg_out + 128 * i, 0, 128);
-  }
-  return HG_OK;
-}
-
 int hg_verify_aggregate(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
                         const uint8_t* sigs, int32_t* codes, uint8_t* agg_pk_out) {
-  if (!c || (n && (!reqs || !sigs || !codes))) return HG_ERR_ARG;
+  if (!c || (n && (!reqs || !sigs || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
-  HG_CHECK(c, hipSetDevice(c->device));
-  return aggregate_host(c, reqs, n, words, nwords, sigs, codes, agg_pk_out, true);
+  return aggregate_host_locked(c, reqs, n, words, nwords, sigs, codes, agg_pk_out, true);
+}
+
+int hg_verify_aggregate_msg(hg_ctx* c, const uint8_t* msg, size_t len, const hg_request* reqs, size_t n,
+                            const uint64_t* words, size_t nwords, const uint8_t* sigs, int32_t* codes,
+                            uint8_t* agg_pk_out) {
+  if (!c || (!msg && len) || (n && (!reqs || !sigs || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  int rc = set_message_locked(c, msg, len);
+  if (rc != HG_OK && rc != HG_ERR_HASH_EOF) return rc;
+  if (n == 0) return HG_OK;
+  return aggregate_host_locked(c, reqs, n, words, nwords, sigs, codes, agg_pk_out, true);
+}
+
+int hg_verify_multisig(hg_ctx* c, const uint32_t* bitlens, const uint32_t* word_offsets, size_t n,
+                       const uint64_t* words, size_t nwords, const uint8_t* sigs, int32_t* codes) {
+  if (!c || (n && (!bitlens || !word_offsets || !sigs || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  // crypto.go:121-124: the bitset must span the registry; the rest is
+  // verifySignature over the range [0, N) (crypto.go:125-136)
+  std::vector<hg_request> reqs(n);
+  for (size_t i = 0; i < n; i++) reqs[i] = hg_request{0u, bitlens[i], (uint32_t)c->nreg, word_offsets[i]};
+  int rc = aggregate_host_locked(c, reqs.data(), n, words, nwords, sigs, codes, nullptr, true);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; i++)
+    if (bitlens[i] != c->nreg) codes[i] = HG_ERR_MULTI_SIZES;
+  return HG_OK;
 }
 
 int hg_aggregate_pk(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
                     uint8_t* agg_pk_out, int32_t* codes) {
-  if (!c || (n && (!reqs || !agg_pk_out || !codes))) return HG_ERR_ARG;
+  if (!c || (n && (!reqs || !agg_pk_out || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
-  HG_CHECK(c, hipSetDevice(c->device));
-  return aggregate_host(c, reqs, n, words, nwords, nullptr, codes, agg_pk_out, false);
+  return aggregate_host_locked(c, reqs, n, words, nwords, nullptr, codes, agg_pk_out, false);
 }
 
 int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out, int32_t* codes) {
-  if (!c || (n && (!a || !b || !out || !codes))) return HG_ERR_ARG;
+  if (!c || (n && (!a || !b || !out || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
@@ -546,6 +738,7 @@ int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   HG_CHECK(c, c->codes_a.ensure(n));
   HG_CHECK(c, c->codes_b.ensure(n));
   HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, a, n * 64, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, b, n * 64, hipMemcpyHostToDevice, c->stream));
   launch_decode_g1(c->bytes_a.p, (int)n, c->flavor, c->pts1.p, c->codes_a.p, c->stream);
@@ -556,12 +749,13 @@ int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
 
 int hg_combine_g2(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out, int32_t* codes) {
-  if (!c || (n && (!a || !b || !out || !codes))) return HG_ERR_ARG;
+  if (!c || (n && (!a || !b || !out || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
@@ -571,6 +765,7 @@ int hg_combine_g2(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   HG_CHECK(c, c->codes_b.ensure(n));
   HG_CHECK(c, c->codes_c.ensure(n));
   uint8_t* d = c->bytes_a.p;
+  HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipMemcpyAsync(d, a, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(d + n * 128, b, n * 128, hipMemcpyHostToDevice, c->stream));
   launch_decode_g2(d, (int)n, c->flavor, c->pts2.p, c->codes_a.p, c->stream);
@@ -582,22 +777,24 @@ int hg_combine_g2(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, d, n * 128, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
 
 int hg_pair(hg_ctx* c, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t* gt_out, int32_t* codes) {
-  if (!c || (n && (!g1s || !g2s || !gt_out || !codes))) return HG_ERR_ARG;
+  if (!c || (n && (!g1s || !g2s || !gt_out || !codes)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
-  HG_CHECK(c, c->bytes_a.ensure(n * 128 > n * 384 ? n * 128 : n * 384));
+  HG_CHECK(c, c->bytes_a.ensure(n * 384));
   HG_CHECK(c, c->bytes_b.ensure(n * 64));
   HG_CHECK(c, c->pts1.ensure(n));
   HG_CHECK(c, c->pts2.ensure(n));
   HG_CHECK(c, c->codes_a.ensure(n));
   HG_CHECK(c, c->codes_b.ensure(n));
   HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, g2s, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, g1s, n * 64, hipMemcpyHostToDevice, c->stream));
   launch_decode_g2(c->bytes_a.p, (int)n, HG_FLAVOR_GO, c->pts2.p, c->codes_a.p, c->stream);
@@ -608,64 +805,60 @@ int hg_pair(hg_ctx* c, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(gt_out, c->bytes_a.p, n * 384, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
 
 int hg_keygen(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* pks_out) {
-  if (!c || (n && (!scalars_be || !pks_out))) return HG_ERR_ARG;
+  if (!c || (n && (!scalars_be || !pks_out)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 128));
   HG_CHECK(c, c->bytes_b.ensure(n * 32));
   HG_CHECK(c, c->pts2.ensure(n));
+  HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
   launch_g2_mul_base(c->bytes_b.p, (int)n, c->pts2.p, c->stream);
   launch_encode_g2(c->pts2.p, (int)n, c->bytes_a.p, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(pks_out, c->bytes_a.p, n * 128, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
 
 int hg_sign(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out) {
-  if (!c || (n && (!scalars_be || !sigs_out))) return HG_ERR_ARG;
-  if (!c->has_msg) {
-    c->err = "hg_set_message was not called";
-    return HG_ERR_ARG;
-  }
-  if (c->hash_eof) return HG_ERR_HASH_EOF;
-  if (n == 0) return HG_OK;
+  if (!c || (n && (!scalars_be || !sigs_out)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  HG_CHECK(c, hipSetDevice(c->device));
-  HG_CHECK(c, c->bytes_a.ensure(n * 64));
-  HG_CHECK(c, c->bytes_b.ensure(n * 32));
-  HG_CHECK(c, c->pts1.ensure(n));
-  HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
-  launch_g1_mul(c->d_h, c->bytes_b.p, (int)n, c->pts1.p, c->stream);
-  launch_encode_g1(c->pts1.p, (int)n, c->bytes_a.p, c->stream);
-  int rc = check_launch(c);
-  if (rc) return rc;
-  HG_CHECK(c, hipMemcpyAsync(sigs_out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipStreamSynchronize(c->stream));
-  return HG_OK;
+  return sign_locked(c, scalars_be, n, sigs_out);
+}
+
+int hg_sign_msg(hg_ctx* c, const uint8_t* msg, size_t len, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out) {
+  if (!c || (!msg && len) || (n && (!scalars_be || !sigs_out)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  int rc = set_message_locked(c, msg, len);
+  if (rc != HG_OK) return rc;
+  return sign_locked(c, scalars_be, n, sigs_out);
 }
 
 int hg_debug_fp12(hg_ctx* c, int op, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out) {
-  if (!c || (n && (!a || !b || !out))) return HG_ERR_ARG;
+  if (!c || (n && (!a || !b || !out)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 384 * 3));
   uint8_t* d = c->bytes_a.p;
+  HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipMemcpyAsync(d, a, n * 384, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(d + n * 384, b, n * 384, hipMemcpyHostToDevice, c->stream));
   launch_fp12_op(op, d, d + n * 384, (int)n, d + 2 * n * 384, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, d + 2 * n * 384, n * 384, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -675,6 +868,7 @@ int hg_diag_read(hg_ctx* c, uint64_t* out, size_t n) {
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
+  if (c->last_ev) HG_CHECK(c, hipEventSynchronize(c->last_ev));
   return diag_read(out, n) == 0 ? HG_OK : HG_ERR_ARG;
 }
 
@@ -685,40 +879,52 @@ int hg_timing_enable(hg_ctx* c, int on) {
   return HG_OK;
 }
 
-int hg_timing_read(hg_ctx* c, double* total_ms, int* launches) {
-  if (!c || !total_ms || !launches) return HG_ERR_ARG;
+int hg_timing_read_phase(hg_ctx* c, int phase, double* total_ms, int* launches) {
+  if (!c || !total_ms || !launches || phase < 0 || phase >= HG_NUM_PHASES) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   double tot = 0;
   int k = 0;
-  for (auto& pr : c->verify_events) {
+  auto& ev = c->events[phase];
+  int rc = HG_OK;
+  for (auto& pr : ev) {
     float ms = 0;
-    HG_CHECK(c, hipEventSynchronize(pr.second));
-    HG_CHECK(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+    hipError_t e = hipEventSynchronize(pr.second);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, pr.first, pr.second);
+    if (e != hipSuccess && rc == HG_OK) {
+      c->err = std::string("hg_timing_read_phase: ") + hipGetErrorString(e);
+      rc = HG_ERR_DEVICE;
+    }
     tot += ms;
     k++;
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
-  c->verify_events.clear();
+  ev.clear();
   *total_ms = tot;
   *launches = k;
-  return HG_OK;
+  return rc;
+}
+
+int hg_timing_read(hg_ctx* c, double* total_ms, int* launches) {
+  return hg_timing_read_phase(c, HG_PHASE_VERIFY, total_ms, launches);
 }
 
 int hg_debug_fp_mul(hg_ctx* c, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out) {
-  if (!c || (n && (!a || !b || !out))) return HG_ERR_ARG;
+  if (!c || (n && (!a || !b || !out)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 32 * 3));
   uint32_t* da = (uint32_t*)c->bytes_a.p;
+  HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipMemcpyAsync(da, a, n * 32, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(da + 8 * n, b, n * 32, hipMemcpyHostToDevice, c->stream));
   launch_fp_mul(da, da + 8 * n, (int)n, da + 16 * n, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, da + 16 * n, n * 32, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, end(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }

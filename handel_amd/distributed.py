@@ -48,3 +48,27 @@ def gather_verdicts(bits: torch.Tensor, world: int, out: List[torch.Tensor] = No
         return out
     dist.all_gather(out, bits)
     return out
+
+
+def verify_sharded(verify_fn, n: int, rank: int, world: int, device=None) -> torch.Tensor:
+    """Sharded verification of one batch of n independent checks: this rank
+    verifies the contiguous slice shard_range(n, rank, world) with
+    verify_fn(lo, hi) -> int32 codes (on `device`), packs its verdicts and
+    all-gathers every rank's bitset (slices differ by at most one check, so
+    bitsets are padded to the largest). Returns the n verdicts of the whole
+    batch (bool, check i valid), in batch order, on every rank."""
+    lo, hi = shard_range(n, rank, world)
+    codes = verify_fn(lo, hi)
+    if device is None:
+        device = codes.device
+    width = (-(-n // world) + 7) // 8
+    bits = torch.zeros(width, dtype=torch.uint8, device=device)
+    if hi > lo:
+        mine = pack_verdicts(codes.to(device))
+        bits[:mine.numel()] = mine
+    got = gather_verdicts(bits, world)
+    parts = []
+    for r in range(world):
+        a, b = shard_range(n, r, world)
+        parts.append(unpack_verdicts(got[r], b - a))
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=torch.bool)

@@ -71,6 +71,11 @@ class Engine:
     def code_string(self, code: int) -> str:
         return self.L.hg_code_string(int(code), self.flavor).decode()
 
+    def processing_error_string(self, code: int) -> str:
+        """The text processing.go's verifySignature returns for `code`
+        (hg_processing_error_string): VerifySignature errors wrapped "handel: ..."."""
+        return self.L.hg_processing_error_string(int(code), self.flavor).decode()
+
     # ----------------------------------------------------------- setup
     def set_message(self, msg: bytes) -> int:
         """hashedMessage once per message; returns HG_OK or HG_ERR_HASH_EOF."""
@@ -96,6 +101,19 @@ class Engine:
         self._check(self.L.hg_verify_batch(self.ctx, _ptr(a), _ptr(b), n, _ptr(codes)), "hg_verify_batch")
         return codes
 
+    def verify_batch_msg(self, msg: bytes, pks: bytes, sigs: bytes) -> np.ndarray:
+        """PublicKey.VerifySignature(msg, sig) x n, hashing and verifying under
+        one lock hold of the context (hg_verify_batch_msg)."""
+        m, a, b = _u8(msg), _u8(pks), _u8(sigs)
+        n = len(b) // 64
+        if len(a) != 128 * n:
+            raise ValueError("pks must hold 128 bytes per signature")
+        codes = np.zeros(n, dtype=np.int32)
+        rc = self.L.hg_verify_batch_msg(self.ctx, _ptr(m) if len(m) else None, len(m), _ptr(a) if n else None,
+                                        _ptr(b) if n else None, n, _ptr(codes) if n else None)
+        self._check(rc, "hg_verify_batch_msg")
+        return codes
+
     def verify_batch_device(self, d_pks: int, d_sigs: int, n: int, d_codes: int, stream: int = 0):
         self._check(self.L.hg_verify_batch_device(self.ctx, d_pks, d_sigs, n, d_codes, stream or None),
                     "hg_verify_batch_device")
@@ -117,6 +135,19 @@ class Engine:
                                                len(words), _ptr(s), _ptr(codes), _ptr(agg)),
                     "hg_verify_aggregate")
         return (codes, agg.tobytes()) if want_agg else codes
+
+    def verify_multisig(self, bitlens, word_offsets, words: np.ndarray, sigs: bytes) -> np.ndarray:
+        """VerifyMultiSignature (crypto.go:120-137) x n (hg_verify_multisig)."""
+        bl = np.ascontiguousarray(bitlens, dtype=np.uint32)
+        wo = np.ascontiguousarray(word_offsets, dtype=np.uint32)
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        s = _u8(sigs)
+        n = len(bl)
+        codes = np.zeros(n, dtype=np.int32)
+        if n:
+            self._check(self.L.hg_verify_multisig(self.ctx, _ptr(bl), _ptr(wo), n, _ptr(words) if len(words) else None,
+                                                  len(words), _ptr(s), _ptr(codes)), "hg_verify_multisig")
+        return codes
 
     def verify_aggregate_device(self, d_reqs: int, n: int, d_words: int, d_sigs: int, d_codes: int,
                                 d_agg: int = 0, stream: int = 0):
@@ -172,6 +203,16 @@ class Engine:
         self._check(self.L.hg_sign(self.ctx, _ptr(s), n, _ptr(out)), "hg_sign")
         return out.tobytes()
 
+    def sign_msg(self, msg: bytes, scalars_be: bytes) -> bytes:
+        """SecretKey.Sign(msg) x n under one lock hold (hg_sign_msg); raises on EOF."""
+        m, sc = _u8(msg), _u8(scalars_be)
+        n = len(sc) // 32
+        out = np.zeros(n * 64, dtype=np.uint8)
+        rc = self.L.hg_sign_msg(self.ctx, _ptr(m) if len(m) else None, len(m), _ptr(sc) if n else None, n,
+                                _ptr(out) if n else None)
+        self._check(rc, "hg_sign_msg")
+        return out.tobytes()
+
     def fp12_op(self, op: int, a: bytes, b: bytes = None) -> bytes:
         """Team Fp12 building-block probe (hg_debug_fp12); 384-byte GT marshals."""
         x = _u8(a)
@@ -196,6 +237,13 @@ class Engine:
         ms = ctypes.c_double()
         k = ctypes.c_int()
         self._check(self.L.hg_timing_read(self.ctx, ctypes.byref(ms), ctypes.byref(k)), "hg_timing_read")
+        return ms.value, k.value
+
+    def timing_read_phase(self, phase: int) -> Tuple[float, int]:
+        ms = ctypes.c_double()
+        k = ctypes.c_int()
+        self._check(self.L.hg_timing_read_phase(self.ctx, int(phase), ctypes.byref(ms), ctypes.byref(k)),
+                    "hg_timing_read_phase")
         return ms.value, k.value
 
     def sync(self):

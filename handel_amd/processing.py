@@ -75,7 +75,9 @@ class BatchVerifier:
             elif c == HG_OK:
                 out.append(None)
             else:
-                out.append("handel: " + self.eng.code_string(int(c)))
+                # processing.go:350-352 returns the level error as is; only
+                # VerifySignature's errors are wrapped "handel: ..." (:361-365)
+                out.append(self.eng.processing_error_string(int(c)))
         return out
 
     def verify_packets(self, packets: Sequence[Tuple[int, bytes]]) -> List[Optional[str]]:
@@ -106,8 +108,22 @@ class BatchVerifier:
         return self.eng.verify_aggregate(*self._pack(items))
 
     def verify_multisignature(self, bits: Sequence[bool], sig: bytes) -> Optional[str]:
-        """crypto.go:120-137 VerifyMultiSignature over the whole registry."""
-        if len(bits) != self.n:
-            return "verify multisignature: inconsistent sizes"
-        c = self.verify_ranges([(0, self.n, bits, sig)])[0]
-        return None if c == HG_OK else self.eng.code_string(int(c))
+        """crypto.go:120-137 VerifyMultiSignature over the whole registry
+        (hg_verify_multisig: the size check and its error text are the C ABI's)."""
+        return self.verify_multisignatures([(bits, sig)])[0]
+
+    def verify_multisignatures(self, items) -> List[Optional[str]]:
+        """VerifyMultiSignature for each (bits, sig) in one GPU batch."""
+        words, bitlens, woffs, sigs = [], [], [], bytearray()
+        nw = 0
+        for bits, sig in items:
+            w = part.bits_to_words(bits)
+            words.append(w)
+            bitlens.append(len(bits))
+            woffs.append(nw)
+            nw += len(w)
+            s = bytes(sig)
+            sigs += s[:64].ljust(64, b"\x00") if len(s) != 64 else s
+        allw = np.concatenate(words) if words else np.zeros(0, dtype=np.uint64)
+        codes = self.eng.verify_multisig(bitlens, woffs, allw, bytes(sigs))
+        return [None if c == HG_OK else self.eng.code_string(int(c)) for c in codes]

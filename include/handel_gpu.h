@@ -7,7 +7,10 @@
  * the Python host package handel_amd binds it with ctypes. Plain pointers
  * and sizes only; every entry point is thread-safe per context (a mutex
  * serialises submitters, matching the concurrent Handel instances of
- * simul/node/main.go:63-77).
+ * simul/node/main.go:63-77). Work submitted on one context runs in
+ * submission order even across HIP streams: each asynchronous submission
+ * records an event, and the next submission on another stream waits for it,
+ * because the submissions share the context's device workspaces.
  *
  * Byte formats are the reference's marshals:
  *   G1 (signature)  64 B  = x || y, 32-byte big-endian affine coords, zeros = infinity
@@ -38,6 +41,11 @@ enum hg_code {
   HG_ERR_CF_EXCEEDS = 7,    /* cloudflare: "bn256: coordinate exceeds modulus" */
   HG_ERR_CF_MALFORMED = 8,  /* cloudflare: "bn256: malformed point" */
   HG_ERR_CF_SHORT = 9,      /* cloudflare: "bn256: not enough data" */
+  /* cloudflare SigBLS.UnmarshalBinary wraps the G1 error (bn256/cf/bn256.go:183-190) */
+  HG_ERR_SIG_CF_EXCEEDS = 10,   /* "bn256: multisig can't unmarshal: bn256: coordinate exceeds modulus" */
+  HG_ERR_SIG_CF_MALFORMED = 11, /* "bn256: multisig can't unmarshal: bn256: malformed point" */
+  HG_ERR_SIG_CF_SHORT = 12,     /* "bn256: multisig can't unmarshal: bn256: not enough data" */
+  HG_ERR_MULTI_SIZES = 13,  /* "verify multisignature: inconsistent sizes"  crypto.go:122-124 */
   HG_ERR_ARG = 100,         /* bad argument to this API */
   HG_ERR_DEVICE = 101       /* HIP runtime failure (see hg_last_error) */
 };
@@ -68,18 +76,32 @@ int hg_create(int device, int flavor, hg_ctx** out);
 void hg_destroy(hg_ctx* ctx);
 const char* hg_last_error(hg_ctx* ctx);
 const char* hg_code_string(int code, int flavor);
+/* The error text processing.go's verifySignature returns for a per-request
+ * code (processing.go:342-368): VerifySignature's errors (signature invalid,
+ * hash EOF) wrapped as "handel: <err>", the level check's own text unwrapped,
+ * everything else as hg_code_string. "" for HG_OK. */
+const char* hg_processing_error_string(int code, int flavor);
 int hg_version(void);
 
 /* Registry.Identities(...).PublicKey() source: uploads n marshalled G2
  * public keys (PublicKey.UnmarshalBinary, bn256/go/bn256.go:113-120), decoding
  * them on the GPU. codes (nullable, n entries) receives per-key decode codes;
- * returns HG_OK only if every key decoded. */
+ * returns HG_OK only if every key decoded. On any failure the context is
+ * left with NO registry (size 0): every aggregate request then fails its
+ * range check instead of reading tables of another registry. */
 int hg_registry_load(hg_ctx* ctx, const uint8_t* pks, size_t n, int32_t* codes);
 size_t hg_registry_size(hg_ctx* ctx);
 
 /* hashedMessage (bn256/go/bn256.go:210-218) computed once per message and
  * cached on the device. Returns HG_OK or HG_ERR_HASH_EOF. */
 int hg_set_message(hg_ctx* ctx, const uint8_t* msg, size_t len);
+
+/* PublicKey.VerifySignature(msg, sig) x n with the message given per call
+ * (bn256/go/bn256.go:82-94): hashing (cached when msg equals the context's
+ * current message) and verification happen under ONE lock hold, so
+ * concurrent callers with different messages cannot interleave. */
+int hg_verify_batch_msg(hg_ctx* ctx, const uint8_t* msg, size_t len, const uint8_t* pks, const uint8_t* sigs,
+                        size_t n, int32_t* codes);
 
 /* n independent PublicKey.VerifySignature(msg, sig) checks (bn256/go:82-94;
  * simul/p2p/aggregator.go:244). pks: n*128 B, sigs: n*64 B, codes: n. */
@@ -102,6 +124,21 @@ int hg_pack_verdicts_device(hg_ctx* ctx, const int32_t* d_codes, size_t n, uint8
  * agg_pk_out (nullable): n*128 B marshal of each aggregate public key. */
 int hg_verify_aggregate(hg_ctx* ctx, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
                         const uint8_t* sigs, int32_t* codes, uint8_t* agg_pk_out);
+
+/* hg_verify_aggregate with the message given per call: hashing (cached when
+ * msg equals the context's current message) and the batch under ONE lock
+ * hold, for callers that share a context across messages. */
+int hg_verify_aggregate_msg(hg_ctx* ctx, const uint8_t* msg, size_t len, const hg_request* reqs, size_t n,
+                            const uint64_t* words, size_t nwords, const uint8_t* sigs, int32_t* codes,
+                            uint8_t* agg_pk_out);
+
+/* VerifyMultiSignature (crypto.go:120-137) x n: request i's bitset of
+ * bitlens[i] bits at words[word_offsets[i] ...] must span the whole registry
+ * (bitlens[i] != registry size -> HG_ERR_MULTI_SIZES, the reference's
+ * "verify multisignature: inconsistent sizes"). The reference's "registry
+ * returned empty identity" cannot occur: the registry is dense. */
+int hg_verify_multisig(hg_ctx* ctx, const uint32_t* bitlens, const uint32_t* word_offsets, size_t n,
+                       const uint64_t* words, size_t nwords, const uint8_t* sigs, int32_t* codes);
 
 /* Device-resident variant (reqs, words, sigs, codes, agg out on the device). */
 int hg_verify_aggregate_device(hg_ctx* ctx, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
@@ -130,16 +167,26 @@ int hg_pair(hg_ctx* ctx, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8
  * the message cannot be hashed). */
 int hg_keygen(hg_ctx* ctx, const uint8_t* scalars_be, size_t n, uint8_t* pks_out);
 int hg_sign(hg_ctx* ctx, const uint8_t* scalars_be, size_t n, uint8_t* sigs_out);
+/* SecretKey.Sign(msg) x n with the message given per call (one lock hold,
+ * like hg_verify_batch_msg). */
+int hg_sign_msg(hg_ctx* ctx, const uint8_t* msg, size_t len, const uint8_t* scalars_be, size_t n,
+                uint8_t* sigs_out);
 
 /* Self test of the field multiplier: out = a*b mod p on plain 256-bit
  * little-endian 32-bit words (8 per element). */
 int hg_debug_fp_mul(hg_ctx* ctx, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out);
 
-/* Measurement hooks: when enabled, every launch of the pairing-check kernel
- * is bracketed by HIP events on the stream it runs on; hg_timing_read
- * returns (and clears) the summed kernel time and the number of launches. */
+/* Measurement hooks: when enabled, device work is bracketed by HIP events on
+ * the stream it runs on, per phase: HG_PHASE_VERIFY = every launch of the
+ * pairing-check kernel, HG_PHASE_AGGREGATE = the Combine fold of an aggregate
+ * submission (plan, order, fold, finish), HG_PHASE_SUBMIT = a whole
+ * verification submission (decode/aggregate + check). hg_timing_read_phase
+ * returns (and clears) the summed time and the count of bracketed intervals;
+ * hg_timing_read is hg_timing_read_phase(HG_PHASE_VERIFY). */
+enum hg_phase { HG_PHASE_VERIFY = 0, HG_PHASE_AGGREGATE = 1, HG_PHASE_SUBMIT = 2, HG_NUM_PHASES = 3 };
 int hg_timing_enable(hg_ctx* ctx, int on);
 int hg_timing_read(hg_ctx* ctx, double* total_ms, int* launches);
+int hg_timing_read_phase(hg_ctx* ctx, int phase, double* total_ms, int* launches);
 
 /* Parity probe of the team Fp12 building blocks: elements are 384-byte GT
  * marshals. op: 0 a*b, 1 a^2, 2 cyclotomic a^2, 3 a^p, 4 a^(p^2), 5 a^-1,

@@ -40,3 +40,27 @@ def test_version_and_code_strings_without_gpu():
     assert L.hg_code_string(3, 0) == b"handel: inconsistent bitset with given level"
     assert L.hg_code_string(2, 0) == b"EOF"
     assert L.hg_code_string(7, 1) == b"bn256: coordinate exceeds modulus"
+
+
+def test_exact_error_strings_without_gpu():
+    """Every code's text (hg_code_string) and the verifySignature wrapping
+    (hg_processing_error_string), against the reference's error values."""
+    L = _lib.load(build_if_missing=False)
+    go, cf = _lib.HG_FLAVOR_GO, _lib.HG_FLAVOR_CF
+    code = lambda c, f=go: L.hg_code_string(c, f).decode()  # noqa: E731
+    proc = lambda c, f=go: L.hg_processing_error_string(c, f).decode()  # noqa: E731
+    assert code(_lib.HG_OK) == "" and proc(_lib.HG_OK) == ""
+    # bn256/go/bn256.go:91,117,186; processing.go:351; crypto.go:123
+    assert code(_lib.HG_ERR_PK_UNMARSHAL) == "unable to unmarshal"
+    assert code(_lib.HG_ERR_SIG_UNMARSHAL) == "bn256: multisig can't unmarshal"
+    assert code(_lib.HG_ERR_MULTI_SIZES) == "verify multisignature: inconsistent sizes"
+    # cloudflare wraps the G1 error in SigBLS.UnmarshalBinary (bn256/cf/bn256.go:183-190)
+    assert code(_lib.HG_ERR_SIG_CF_EXCEEDS, cf) == "bn256: multisig can't unmarshal: bn256: coordinate exceeds modulus"
+    assert code(_lib.HG_ERR_SIG_CF_MALFORMED, cf) == "bn256: multisig can't unmarshal: bn256: malformed point"
+    assert code(_lib.HG_ERR_SIG_CF_SHORT, cf) == "bn256: multisig can't unmarshal: bn256: not enough data"
+    assert code(_lib.HG_ERR_CF_MALFORMED, cf) == "bn256: malformed point"
+    # processing.go:361-365 wraps VerifySignature's errors; the level error is returned as is (:350-352)
+    assert proc(_lib.HG_ERR_SIG_INVALID) == "handel: bn256: signature invalid"
+    assert proc(_lib.HG_ERR_HASH_EOF) == "handel: EOF"
+    assert proc(_lib.HG_ERR_LEVEL) == "handel: inconsistent bitset with given level"
+    assert "handel: handel:" not in "".join(proc(c) for c in range(14))

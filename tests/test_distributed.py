@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from handel_amd.distributed import gather_verdicts, pack_verdicts, shard_range, unpack_verdicts
+from handel_amd.distributed import gather_verdicts, pack_verdicts, shard_range, unpack_verdicts, verify_sharded
 
 
 def test_shard_range_covers_batch():
@@ -65,3 +65,45 @@ def test_two_rank_gloo_gather():
     res = sorted(q.get(timeout=10) for _ in range(world))
     for rank, valid, total in res:
         assert total == 4096 and valid == 4096 - 512
+
+
+def _pattern(i: int) -> int:
+    """A verdict code that depends on the global check index (rank-distinct
+    slices get distinct patterns, so a misordered gather shows)."""
+    return 0 if (i * 2654435761) % 7 < 4 else 1 + i % 3
+
+
+def _sharded_worker(rank, world, port, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seen = []
+
+    def verify(lo, hi):
+        seen.append((lo, hi))
+        return torch.tensor([_pattern(i) for i in range(lo, hi)], dtype=torch.int32)
+
+    full = verify_sharded(verify, n, rank, world, device=torch.device("cpu"))
+    q.put((rank, seen, full.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 4096), (3, 4097), (3, 5)])
+def test_sharded_gather_order(world, n):
+    """verify_sharded at world 2 and 3 over gloo: every rank verifies exactly
+    its contiguous slice, and every rank ends with the whole batch's verdicts
+    in batch order (uneven slices included)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    want = [_pattern(i) == 0 for i in range(n)]
+    for rank, seen, full in res:
+        assert seen == [shard_range(n, rank, world)]
+        assert full == want

@@ -284,32 +284,39 @@ def test_empty_batches(engine):
     assert engine.keygen(b"") == b"" and engine.sign(b"") == b""
 
 
-def test_full_size_ragged_batch_matches_oracle(engine):
+@pytest.mark.parametrize("flavor", ["go", "cf"])
+def test_full_size_ragged_batch_matches_oracle(request, flavor):
     """BASELINE config 2 at full size plus a ragged tail (4100 checks: more
     teams than one wave per SIMD holds, last workgroup partly filled), every
-    verdict against the C restatement of the reference algorithm."""
+    verdict against the C restatement of the reference algorithm, under both
+    upstream flavors' decode rules (cf: the default curve of every shipped
+    simul config)."""
     import bench
 
+    engine = request.getfixturevalue("engine" if flavor == "go" else "engine_cf")
     n = 4100
     pks, sigs, expect = bench.make_batch(engine, n, seed=99)
     assert engine.set_message(F.LIB_MESSAGE) == 0
     got = engine.verify_batch(pks, sigs)
-    want = R.verify_batch(F.LIB_MESSAGE, pks, sigs, nthreads=16)
+    want = R.verify_batch(F.LIB_MESSAGE, pks, sigs, nthreads=16, flavor=0 if flavor == "go" else 1)
     assert np.array_equal(got, want)
     assert np.array_equal(got, expect)  # exactly the tampered 1/8 fail
 
 
+@pytest.mark.parametrize("flavor", ["go", "cf"])
 @pytest.mark.parametrize("full", [False, True], ids=["levels", "full_registry"])
-def test_full_size_aggregate_matches_oracle(engine, full):
+def test_full_size_aggregate_matches_oracle(request, full, flavor):
     """BASELINE config 3 at full size: 4096 multisigs on a 4000-key registry
     (random Handel levels, or VerifyMultiSignature over the whole registry),
-    verdicts and aggregate-key marshals byte-exact against the C restatement."""
+    verdicts and aggregate-key marshals byte-exact against the C restatement,
+    under both upstream flavors (cf decodes the registry with its subgroup
+    check)."""
     import bench
 
+    engine = request.getfixturevalue("engine" if flavor == "go" else "engine_cf")
     n, n_reg = 4096, 4000
     assert engine.set_message(F.LIB_MESSAGE) == 0
-    reqs, words, sigs, expect, _ = bench.make_aggregate_batch(engine, n_reg, n, seed=77, full=full)
-    reg = engine.keygen(bench.seeded_scalars(n_reg, 77))  # the registry make_aggregate_batch loaded
+    reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(engine, n_reg, n, seed=77, full=full)
     codes, agg = engine.verify_aggregate(reqs, words, sigs, want_agg=True)
     assert np.array_equal(codes, expect)  # exactly the tampered 1/8 fail
     want, want_agg = R.verify_aggregate(F.LIB_MESSAGE, reg, reqs["offset"], reqs["bitlen"], reqs["level_size"],

@@ -61,8 +61,10 @@ def test_golden_registry_and_packets(engine):
     packets.append((1, b"\x00"))                                   # truncated length prefix
     packets.append((1, bytes.fromhex(ms["requests"][0]["multisig"])[:-1]))  # short signature
     got = bv.verify_packets(packets)
+    want_text = {0: None, 1: "handel: bn256: signature invalid", 3: "handel: inconsistent bitset with given level",
+                 6: "runtime error: invalid memory address or nil pointer dereference"}
     for r, g in zip(reqs, got):
-        assert (g is None) == (r["code"] == 0), (r["level"], r["code"], g)
+        assert g == want_text[r["code"]], (r["level"], r["code"], g)
     assert got[-2] == "EOF"
     assert got[-1] == "bn256: multisig can't unmarshal"
 
@@ -79,3 +81,28 @@ def test_generate_records_match_oracle(engine):
         assert err is None
         assert rec.private == REG.secret_marshal(k).hex()
         assert rec.public == O.g2_marshal(O.g2_mul(O.G2_GEN, k)).hex()
+
+
+@pytest.mark.gpu
+def test_verify_multisignature_errors(engine):
+    """VerifyMultiSignature (crypto.go:120-137) through hg_verify_multisig: the
+    full-registry request of the golden set verifies, a bitset of the wrong
+    length gets the reference's "inconsistent sizes" text, a tampered
+    signature the unwrapped VerifySignature error."""
+    from handel_amd import partitioner as part
+    from handel_amd.processing import BatchVerifier
+
+    with open(os.path.join(GOLD, "bn256_vectors.json")) as f:
+        ms = json.load(f)["multisig"]
+    recs = REG.read_records(os.path.join(GOLD, "registry_50.csv"))
+    bv = BatchVerifier(engine, REG.registry_bytes(recs), bytes.fromhex(ms["msg"]), node_id=ms["node"])
+    full = [r for r in ms["requests"] if r["level"] is None][0]
+    bits, sig = part.multisig_unmarshal(bytes.fromhex(full["multisig"]))
+    bits = [bool(b) for b in bits]
+    assert len(bits) == 50 and sig == bytes.fromhex(full["agg_sig"])
+    bad = bytearray(sig)
+    bad[5] ^= 1
+    got = bv.verify_multisignatures([(bits, sig), (bits[:-1], sig), (bits + [True], sig), (bits, bytes(bad))])
+    assert got[0] is None
+    assert got[1] == got[2] == "verify multisignature: inconsistent sizes"
+    assert got[3] in ("bn256: multisig can't unmarshal", "bn256: signature invalid")
