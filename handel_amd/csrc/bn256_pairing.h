@@ -45,10 +45,10 @@ HG_DEV void team_final_exp(const Team& T, uint32_t* F, XStream& S) {
   t12_frob2(T, S_B, S_F);                                       // fp2
   x_mul12<S_A, S_A, S_B>(T, S, xh<IMul12<S_A, S_A, S_B>>());
   t12_frob(T, S_B, S_B);                                        // fp3
-  x_mul12<S_A, S_A, S_B>(T, S, xh<ICyc<S_J, S_F>>());          // y0 = fp * fp2 * fp3
+  x_mul12<S_A, S_A, S_B>(T, S, xh<ICyc<S_C, S_F>>());          // y0 = fp * fp2 * fp3
   DIAG_ADD(6);
-  t12_pow_u_x<S_C, S_F>(T, S, xh<ICyc<S_J, S_C>>());           // fu
-  t12_pow_u_x<S_D, S_C>(T, S, xh<ICyc<S_J, S_D>>());           // fu2
+  t12_pow_u_x<S_C, S_F>(T, S, xh<ICyc<S_D, S_C>>());           // fu
+  t12_pow_u_x<S_D, S_C>(T, S, xh<ICyc<S_E, S_D>>());           // fu2
   t12_pow_u_x<S_E, S_D>(T, S, xh<IMul12<S_H, S_C, S_H>>());    // fu3
   DIAG_ADD(7);
   t12_frob(T, S_G, S_C);

@@ -269,38 +269,41 @@ template <int PROG>
 HG_DEV void x_g2(const Team& T, XStream& S, XHint h) { IG2<PROG>::run(T, S, h); }
 
 
-__constant__ static const int8_t kUNaf3X[kUNaf3Len] = HG_U_NAF3;
-
-// the program that multiplies by digit d (d != 0) in t12_pow_u_x
-template <int D, int SA>
-HG_DEV XHint pow_u_mul_hint(int d) {
-  return d == 1 ? xh<IMul12<D, D, SA>>() : d == 3 ? xh<IMul12<D, D, S_J>>()
-       : d == -1 ? xh<IMul12<D, D, S_K>>() : xh<IMul12<D, D, S_L>>();
+// N cyclotomic squarings of D in place; h: the program that runs after them
+template <int D, int N>
+HG_DEV void x_cyc_sqr_n(const Team& T, XStream& S, XHint h) {
+  x_for<N>([&](auto i) { x_cyc_sqr<D, D>(T, S, i + 1 < N ? xh<ICyc<D, D>>() : h); });
 }
 
-// dst = a^u (x/crypto gfP12.Exp(t, u)) for a in the cyclotomic subgroup, where
-// a^-1 = conj(a): width-3 signed digits of u (62 cyclotomic squarings and 16
-// multiplications instead of 62 + 29). Scratch slots: J = a^3, K = a^-1,
-// L = a^-3 (dst, SA not among them). h: the program that runs after it.
+// dst = a^v for a in the cyclotomic subgroup (a^-1 = conj(a)), where v =
+// 1868033 = 2^21 - 2^18 + 2^15 + 2^8 + 1 is the cube root of the BN
+// parameter u (u = v^3): 21 cyclotomic squarings and 4
+// multiplications, scratch slot K = a^-1. h: the program that runs after it.
+template <int D, int SA>
+HG_DEV void t12_pow_v_x(const Team& T, XStream& S, XHint h) {
+  static_assert(D != SA && D != S_K && SA != S_K, "scratch slot");
+  t12_conj(T, S_K, SA);                                        // a^-1
+  x_cyc_sqr<D, SA>(T, S, xh<ICyc<D, D>>());                    // a^2
+  x_cyc_sqr_n<D, 2>(T, S, xh<IMul12<D, D, S_K>>());            // a^8
+  x_mul12<D, D, S_K>(T, S, xh<ICyc<D, D>>());                  // a^7      (2^3 - 1)
+  x_cyc_sqr_n<D, 3>(T, S, xh<IMul12<D, D, SA>>());             // a^56
+  x_mul12<D, D, SA>(T, S, xh<ICyc<D, D>>());                   // a^57     (2^6 - 2^3 + 1)
+  x_cyc_sqr_n<D, 7>(T, S, xh<IMul12<D, D, SA>>());
+  x_mul12<D, D, SA>(T, S, xh<ICyc<D, D>>());                   // a^7297   (57 * 2^7 + 1)
+  x_cyc_sqr_n<D, 8>(T, S, xh<IMul12<D, D, SA>>());
+  x_mul12<D, D, SA>(T, S, h);                                  // a^v      (7297 * 2^8 + 1)
+}
+
+// dst = a^u (x/crypto gfP12.Exp(t, u)) for a in the cyclotomic subgroup:
+// three exponentiations by v (u = v^3): 63 cyclotomic squarings and 12
+// multiplications (a width-3 NAF of u needs 62 + 17). Scratch slots J, K
+// (dst, SA not among them). h: the program that runs after it.
 template <int D, int SA>
 HG_DEV void t12_pow_u_x(const Team& T, XStream& S, XHint h) {
-  static_assert(D != S_J && D != S_K && D != S_L && SA != S_J && SA != S_K && SA != S_L, "scratch slots");
-  static_assert(HG_U_NAF3_TOP == 3, "top digit of the width-3 NAF of u");
-  x_cyc_sqr<S_J, SA>(T, S, xh<IMul12<S_J, S_J, SA>>());
-  x_mul12<S_J, S_J, SA>(T, S, xh<ICyc<D, D>>());  // a^3
-  t12_conj(T, S_K, SA);      // a^-1
-  t12_conj(T, S_L, S_J);     // a^-3
-  t12_copy(T, D, S_J);
-  for (int i = kUNaf3Len - 2; i >= 0; i--) {
-    const int d = kUNaf3X[i];  // wave-uniform
-    // after this digit: the next squaring, or the caller's next program
-    const XHint after = i > 0 ? xh<ICyc<D, D>>() : h;
-    x_cyc_sqr<D, D>(T, S, d != 0 ? pow_u_mul_hint<D, SA>(d) : after);
-    if (d == 1) x_mul12<D, D, SA>(T, S, after);
-    else if (d == 3) x_mul12<D, D, S_J>(T, S, after);
-    else if (d == -1) x_mul12<D, D, S_K>(T, S, after);
-    else if (d == -3) x_mul12<D, D, S_L>(T, S, after);
-  }
+  static_assert(D != S_J && D != S_K && SA != S_J && SA != S_K && D != SA, "scratch slots");
+  t12_pow_v_x<D, SA>(T, S, xh<ICyc<S_J, D>>());
+  t12_pow_v_x<S_J, D>(T, S, xh<ICyc<D, S_J>>());
+  t12_pow_v_x<D, S_J>(T, S, h);
 }
 
 // dst = a^-1 (x/crypto gfP12.Invert) with scratch slots S1, S2

@@ -68,6 +68,8 @@ def test_abi_threads_native(engine, tmp_path):
     assert os.path.exists(exe), "build() compiles the harness in-tree"
     reg, reqs, words, sigs, codes, agg = _aggregate_fixture()
     # the harness's expectations are the oracle's; the GPU agrees single-threaded first
+    assert engine.set_message(F.LIB_MESSAGE) == 0
+    assert list(engine.registry_load(reg)) == [0] * 64
     got_codes, got_agg = engine.verify_aggregate(reqs, words, sigs, want_agg=True)
     assert list(got_codes) == list(codes) and got_agg == agg
     d = tmp_path
@@ -195,7 +197,7 @@ def _cf_sig_cases():
     cases.append(good[:32] + (y + O.P).to_bytes(32, "big") if y + O.P < 1 << 256 else good[:32] + b"\xff" * 32)
     cases.append((x ^ 1).to_bytes(32, "big") + good[32:])                # off the curve
     cases.append(b"\xff" * 64)                                           # both >= p
-    cases.append((1).to_bytes(32, "big") + (2).to_bytes(32, "big"))      # small, off the curve
+    cases.append((1).to_bytes(32, "big") + (3).to_bytes(32, "big"))      # small, off the curve
     return cases
 
 
@@ -230,7 +232,7 @@ def test_cf_mirror_unmarshal_text():
     from handel_amd import bn256 as BN
 
     cf, go = BN.NewConstructor("cf"), BN.NewConstructor("go")
-    off = (1).to_bytes(32, "big") + (2).to_bytes(32, "big")
+    off = (1).to_bytes(32, "big") + (3).to_bytes(32, "big")  # 9 != 1 + 3
     with pytest.raises(BN.BN256Error, match="^bn256: multisig can't unmarshal: bn256: malformed point$"):
         cf.Signature().UnmarshalBinary(off)
     with pytest.raises(BN.BN256Error, match="^bn256: multisig can't unmarshal$"):

@@ -295,8 +295,8 @@ def test_full_size_ragged_batch_matches_oracle(request, flavor):
 
     engine = request.getfixturevalue("engine" if flavor == "go" else "engine_cf")
     n = 4100
+    assert engine.set_message(F.LIB_MESSAGE) == 0  # make_batch signs with the context's message
     pks, sigs, expect = bench.make_batch(engine, n, seed=99)
-    assert engine.set_message(F.LIB_MESSAGE) == 0
     got = engine.verify_batch(pks, sigs)
     want = R.verify_batch(F.LIB_MESSAGE, pks, sigs, nthreads=16, flavor=0 if flavor == "go" else 1)
     assert np.array_equal(got, want)

@@ -1009,8 +1009,12 @@ SCR_BASE = {"FE": F_BASE + 2, "ML": 12 * SLOTS.index("C")}
 
 
 def _pow_u_mul_instances(dst, sa):
-    return [("MUL12", ("J", "J", sa))] + [("MUL12", (dst, dst, m)) for m in (sa, "J", "K", "L")] + \
-        [("CYC_SQR_X", ("J", sa)), ("CYC_SQR_X", (dst, dst))]
+    """t12_pow_u_x<dst, sa> (bn256_xprog.h): three exponentiations by v,
+    a -> dst, dst -> J, J -> dst, each with the conjugate of its base in K."""
+    out = []
+    for d, base in ((dst, sa), ("J", dst), (dst, "J")):
+        out += [("CYC_SQR_X", (d, base)), ("CYC_SQR_X", (d, d)), ("MUL12", (d, d, "K")), ("MUL12", (d, d, base))]
+    return out
 
 
 INSTANCES = sorted(set(
