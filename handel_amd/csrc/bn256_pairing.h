@@ -45,11 +45,21 @@ HG_DEV void team_final_exp(const Team& T, uint32_t* F, XStream& S) {
   t12_frob2(T, S_B, S_F);                                       // fp2
   x_mul12<S_A, S_A, S_B>(T, S, xh<IMul12<S_A, S_A, S_B>>());
   t12_frob(T, S_B, S_B);                                        // fp3
-  x_mul12<S_A, S_A, S_B>(T, S, xh<ICyc<S_C, S_F>>());          // y0 = fp * fp2 * fp3
+  x_mul12<S_A, S_A, S_B>(T, S, xh<ICyc<S_J, S_I>>());          // y0 = fp * fp2 * fp3
   DIAG_ADD(6);
-  t12_pow_u_x<S_C, S_F>(T, S, xh<ICyc<S_D, S_C>>());           // fu
-  t12_pow_u_x<S_D, S_C>(T, S, xh<ICyc<S_E, S_D>>());           // fu2
-  t12_pow_u_x<S_E, S_D>(T, S, xh<IMul12<S_H, S_C, S_H>>());    // fu3
+  // fu, fu2, fu3 = t1^u, t1^(u^2), t1^(u^3) as nine exponentiations by v
+  // (u = v^3) ping-ponging between slots I and J: one copy of the program in
+  // the code, run nine times
+  t12_copy(T, S_I, S_F);
+#pragma unroll 1
+  for (int st = 0; st < 9; st++) {
+    const XHint next = st == 8 ? xh<IMul12<S_H, S_C, S_H>>() : (st & 1) ? xh<ICyc<S_J, S_I>>() : xh<ICyc<S_I, S_J>>();
+    if ((st & 1) == 0) t12_pow_v_x<S_J, S_I>(T, S, next);
+    else t12_pow_v_x<S_I, S_J>(T, S, next);
+    if (st == 2) t12_copy(T, S_C, S_J);  // fu
+    if (st == 5) t12_copy(T, S_D, S_I);  // fu2
+    if (st == 8) t12_copy(T, S_E, S_J);  // fu3
+  }
   DIAG_ADD(7);
   t12_frob(T, S_G, S_C);
   t12_conj(T, S_G, S_G);                                        // y3 = conj(frob(fu))
@@ -89,23 +99,20 @@ struct CheckCtx {
   bool use_s;   // sig contributes (not infinity)
 };
 
-// Writes the team's G2 register file: point R = Q (projective, see below), Q, -Qy, Qy^2, the
+// Writes the team's G2 register file: point R = Q (projective, see below), Q, -Qy, the
 // Frobenius images q1 = pi(Q), -q2 = (Qx gamma2[2], Qy) (optate.go miller),
 // the G1 points and constants.
 HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
   const Fp2 g1[6] = HG_GAMMA1;
   const Fp g2[6] = HG_GAMMA2;
-  Fp2 nqy, r2, q1x, q1y, q1r2, q2x, t, one2, zero2;
+  Fp2 nqy, q1x, q1y, q2x, t, one2;
   f2_neg(nqy, C.qy);
-  f2_sqr(r2, C.qy);
   f2_conj(t, C.qx);
   f2_mul(q1x, t, g1[2]);
   f2_conj(t, C.qy);
   f2_mul(q1y, t, g1[3]);
-  f2_sqr(q1r2, q1y);
   f2_muls(q2x, C.qx, g2[2]);
   f2_one(one2);
-  f2_zero(zero2);
   Fp zero, one, nsy;
   fp_zero(zero);
   fp_one(one);
@@ -129,17 +136,12 @@ HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
     put2(R_X_x, xqx);
     put2(R_Y_x, xqy);
     put2(R_Z_x, one2);
-    put2(R_T_x, one2);
     put2(R_QX_x, C.qx);
     put2(R_QY_x, C.qy);
     put2(R_NQY_x, nqy);
-    put2(R_R2_x, r2);
     put2(R_P1X_x, q1x);
     put2(R_P1Y_x, q1y);
-    put2(R_P1R2_x, q1r2);
     put2(R_P2X_x, q2x);
-    put2(R_F2ONE_x, one2);
-    put2(R_F2ZERO_x, zero2);
   }
   team_sync();
 }

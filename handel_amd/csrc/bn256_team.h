@@ -63,11 +63,20 @@ HG_DEV void ld_f2(Fp2& r, const uint32_t* f12, int k) {
   ld_fp(r.y, f12 + (2 * k + 1) * 10);
 }
 
-HG_DEV void team_sync() { __syncthreads(); }  // blocks are exactly one wave
+// Orders a team's LDS traffic: every lane's earlier LDS writes are seen by
+// every lane's later LDS reads. A team lives inside ONE wave, so a wave-level
+// barrier is enough (the LDS serves one wave's requests in issue order; the
+// wait and the memory clobber keep the compiler from moving LDS accesses
+// across it) — and a workgroup barrier would be wrong in k_verify, whose two
+// waves run different programs between their shared barriers.
+HG_DEV void team_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 HG_DEV Team make_team(uint32_t* lds_base, int words_per_team) {
   Team T;
-  int team = threadIdx.x >> 4;
+  int team = (threadIdx.x & 63) >> 4;  // teams are numbered within their wave
   T.tl = threadIdx.x & 15;
   T.base = lds_base + team * words_per_team;
   T.active = T.tl < 12;

@@ -16,13 +16,8 @@ __device__ uint64_t g_diag[4096 * 16];
 
 
 // TEAMS checks per workgroup of 16 * TEAMS lanes (one wave; LDS sized to TEAMS)
-#ifdef HG_WPE2  // experiment: cap registers at 256 so two waves fit on a SIMD
-#define HG_VERIFY_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
-#else
-#define HG_VERIFY_ATTR
-#endif
 template <int TEAMS>
-__global__ __launch_bounds__(64) HG_VERIFY_ATTR void k_verify(const CheckIn* in, int n, const LineCoef* tab,
+__global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const LineCoef* tab,
                                                const PointG1* hpt, int32_t* codes) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
   Team T = make_team(lds, kTeamWords);

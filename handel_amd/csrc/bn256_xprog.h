@@ -40,8 +40,9 @@ struct XHint {
   int off, w;  // table offset and per-lane stride of the round to prefetch (off < 0: none)
 };
 struct XStream;
-template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2, int KP, int KL1, int KL2>
-HG_DEV void x_round(const Team& T, XStream& S, XHint nxt);
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2>
+HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt);
+
 
 }  // namespace hg
 
@@ -201,9 +202,10 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 // then job 1 (NP x (u, v), NL x term, dst) and, in a fused round (NP2 + NL2 >
 // 0), job 2 (NP2 x (u, v), NL2 x term, dst2); padded to W dwords. Both jobs
 // read before either result is stored, so in-place programs are fine.
-template <int NV, int NT, int NP, int NL, int W, int OFF, int NP2, int NL2, int KP, int KL1, int KL2>
-HG_DEV void x_round(const Team& T, XStream& S, XHint nxt) {
-  if (S.off != OFF) x_fetch(T, S, XHint{OFF, W});  // wave-uniform; only without a (correct) hint
+// off: the round's table offset
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2>
+HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
+  if (S.off != off) x_fetch(T, S, XHint{off, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
   x_for<W>([&](auto i) { w[i] = S.w[i]; });
   if (nxt.off >= 0) x_fetch(T, S, nxt);
@@ -269,29 +271,28 @@ template <int PROG>
 HG_DEV void x_g2(const Team& T, XStream& S, XHint h) { IG2<PROG>::run(T, S, h); }
 
 
-// N cyclotomic squarings of D in place; h: the program that runs after them
-template <int D, int N>
-HG_DEV void x_cyc_sqr_n(const Team& T, XStream& S, XHint h) {
-  x_for<N>([&](auto i) { x_cyc_sqr<D, D>(T, S, i + 1 < N ? xh<ICyc<D, D>>() : h); });
-}
-
 // dst = a^v for a in the cyclotomic subgroup (a^-1 = conj(a)), where v =
 // 1868033 = 2^21 - 2^18 + 2^15 + 2^8 + 1 is the cube root of the BN
 // parameter u (u = v^3): 21 cyclotomic squarings and 4
 // multiplications, scratch slot K = a^-1. h: the program that runs after it.
+// The squaring runs are runtime loops (one copy of each program in the code:
+// the final exponentiation is long enough to miss in the instruction cache).
 template <int D, int SA>
 HG_DEV void t12_pow_v_x(const Team& T, XStream& S, XHint h) {
   static_assert(D != SA && D != S_K && SA != S_K, "scratch slot");
-  t12_conj(T, S_K, SA);                                        // a^-1
-  x_cyc_sqr<D, SA>(T, S, xh<ICyc<D, D>>());                    // a^2
-  x_cyc_sqr_n<D, 2>(T, S, xh<IMul12<D, D, S_K>>());            // a^8
-  x_mul12<D, D, S_K>(T, S, xh<ICyc<D, D>>());                  // a^7      (2^3 - 1)
-  x_cyc_sqr_n<D, 3>(T, S, xh<IMul12<D, D, SA>>());             // a^56
-  x_mul12<D, D, SA>(T, S, xh<ICyc<D, D>>());                   // a^57     (2^6 - 2^3 + 1)
-  x_cyc_sqr_n<D, 7>(T, S, xh<IMul12<D, D, SA>>());
-  x_mul12<D, D, SA>(T, S, xh<ICyc<D, D>>());                   // a^7297   (57 * 2^7 + 1)
-  x_cyc_sqr_n<D, 8>(T, S, xh<IMul12<D, D, SA>>());
-  x_mul12<D, D, SA>(T, S, h);                                  // a^v      (7297 * 2^8 + 1)
+  t12_conj(T, S_K, SA);                      // a^-1
+  x_cyc_sqr<D, SA>(T, S, xh<ICyc<D, D>>());  // a^2
+  // segments: squarings, then a multiplication by a^-1 (segment 0) or a:
+  // a^2 -> a^8 -> a^7 -> a^56 -> a^57 -> a^7296 -> a^7297 -> a^(7297 * 256) -> a^v
+  const int nsq[4] = {2, 3, 7, 8};
+#pragma unroll 1
+  for (int seg = 0; seg < 4; seg++) {
+    const XHint mul = seg == 0 ? xh<IMul12<D, D, S_K>>() : xh<IMul12<D, D, SA>>();
+#pragma unroll 1
+    for (int i = 0; i < nsq[seg]; i++) x_cyc_sqr<D, D>(T, S, i + 1 < nsq[seg] ? xh<ICyc<D, D>>() : mul);
+    if (seg == 0) x_mul12<D, D, S_K>(T, S, xh<ICyc<D, D>>());
+    else x_mul12<D, D, SA>(T, S, seg < 3 ? xh<ICyc<D, D>>() : h);
+  }
 }
 
 // dst = a^u (x/crypto gfP12.Exp(t, u)) for a in the cyclotomic subgroup:

@@ -12,9 +12,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
 
 
+def _torch_first():
+    """Initialise torch's HIP runtime before the engine's: tests that move
+    tensors to the GPU then find the device whatever test ran first."""
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.set_device(0)
+        torch.zeros(1, device="cuda")
+
+
 @pytest.fixture(scope="session")
 def engine():
     from handel_amd.engine import Engine
+    _torch_first()
     e = Engine(device=0, flavor="go")
     yield e
     e.close()
@@ -23,6 +34,7 @@ def engine():
 @pytest.fixture(scope="session")
 def engine_cf():
     from handel_amd.engine import Engine
+    _torch_first()
     e = Engine(device=0, flavor="cf")
     yield e
     e.close()

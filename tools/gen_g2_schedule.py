@@ -44,12 +44,19 @@ NONE = 255
 
 # ------------------------------------------------------------------ register file
 FP_SCALARS = ["ZERO", "ONE", "PX", "PY", "SX", "NSY"]
-FP2_REGS = ["X", "Y", "Z", "T", "QX", "QY", "NQY", "R2", "P1X", "P1Y", "P1R2", "P2X",
-            "FA", "FBX", "FCY", "FB", "FC", "LA", "LB", "LC", "F2ONE", "F2ZERO",
-            # doubling temporaries
-            "A", "B", "S", "C", "W", "G", "V", "ET", "ZP", "TPY",
-            # addition temporaries
-            "AB", "S1", "D", "I", "S2", "H", "J", "AV", "L1", "XN", "YJ", "TP", "LA1", "S3"]
+# The kernels' register file (kG2Regs): the projective Miller-loop programs'
+# point, pk, line coefficients and temporaries. FA, FBX, FCY must stay
+# consecutive (load_fixed_line).
+FP2_RUNTIME = ["X", "Y", "Z", "QX", "QY", "NQY", "P1X", "P1Y", "P2X",
+               "FA", "FBX", "FCY", "FB", "FC", "LA", "LB", "LC",
+               # projective doubling temporaries
+               "A", "B", "S", "C", "G",
+               # projective addition temporaries
+               "AB", "S1", "D", "I", "S2", "H", "J", "AV", "L1"]
+# only the Jacobian x/crypto-shaped programs (DBL, ADD_*: generator
+# cross-checks, never run by a kernel) use these; they lie past kG2Regs
+FP2_LEGACY = ["T", "R2", "P1R2", "F2ONE", "F2ZERO", "W", "V", "ET", "ZP", "TPY", "XN", "YJ", "TP", "LA1", "S3"]
+FP2_REGS = FP2_RUNTIME + FP2_LEGACY
 REG = {}
 for i, n in enumerate(FP_SCALARS):
     REG[n] = i
@@ -58,6 +65,7 @@ for i, n in enumerate(FP2_REGS):
     REG[n + ".x"] = _base + 2 * i
     REG[n + ".y"] = _base + 2 * i + 1
 NREGS = _base + 2 * len(FP2_REGS)
+NREGS_RUNTIME = _base + 2 * len(FP2_RUNTIME)
 assert NREGS <= 128
 # Fp12 source slots: Fp2 coefficient k of slot A is "A{k}", of slot B "B{k}"
 for k in range(6):
@@ -169,9 +177,9 @@ def xi_terms(slots_x, slots_y, c):
 
 
 # ------------------------------------------------------------------ programs
-def fixed_line_eval():
-    # FB = FBX * SX, FC = FCY * NSY  (the G2Base line at -sig)
-    return smul("FB", [("FBX", 1)], "SX") + smul("FC", [("FCY", 1)], "NSY")
+def fixed_line_eval(sfx=""):
+    # FB = FBX * SX, FC = FCY * NSY  (the G2Base line at -sig), line set sfx
+    return smul("FB" + sfx, [("FBX" + sfx, 1)], "SX") + smul("FC" + sfx, [("FCY" + sfx, 1)], "NSY")
 
 
 def prog_double():
@@ -232,7 +240,7 @@ def _xi_lc(name):
     return [(x, 3), (y, 1)], [(y, 3), (x, -1)]
 
 
-def prog_double_proj():
+def prog_double_proj(sfx=""):
     """T = (X : Y : xi W) -> 2T (scaled by 4) and the tangent line at (PX, PY):
        XY, B = Y^2, U = 9 xi W^2 (= 3 b' Z^2), YW, X2 = X^2
        X' = 2 XY (B - 3U), Y' = (B + 3U)^2 - 12 U^2, W' = 8 B YW
@@ -241,17 +249,18 @@ def prog_double_proj():
     u = [Lane(comp(PD["U"], "x"), [([(wx, 6)], [(wy, 9)]), ([(wy, 9), (wx, 9)], [(wy, 1), (wx, -1)])]),
          Lane(comp(PD["U"], "y"), [([(wy, 9), (wx, 9)], [(wy, 3), (wx, -3)]), ([(wx, -18)], [(wy, 1)])])]
     r1 = (mul(PD["XY"], [("X", 1)], [("Y", 1)]) + sq(PD["B"], [("Y", 1)]) + u
-          + mul(PD["YW"], [("Y", 1)], [("Z", 1)]) + sq(PD["X2"], [("X", 1)]) + fixed_line_eval())
+          + mul(PD["YW"], [("Y", 1)], [("Z", 1)]) + sq(PD["X2"], [("X", 1)]) + fixed_line_eval(sfx))
     b, uu = PD["B"], PD["U"]
     y3 = [Lane(comp("Y", c), sq_terms([(b, 1), (uu, 3)], c) + sq_terms([(uu, 1)], c, k=-12)) for c in "xy"]
     cx, cy = _xi_lc(PD["YW"])
-    lc = [Lane(comp("LC", "x"), [(scale(cx, -2), scal("PY"))]), Lane(comp("LC", "y"), [(scale(cy, -2), scal("PY"))])]
+    lc = [Lane(comp("LC" + sfx, "x"), [(scale(cx, -2), scal("PY"))]),
+          Lane(comp("LC" + sfx, "y"), [(scale(cy, -2), scal("PY"))])]
     r2 = (mul("X", [(PD["XY"], 2)], [(b, 1), (uu, -3)]) + y3 + mul("Z", [(b, 8)], [(PD["YW"], 1)])
-          + lc + smul("LB", [(PD["X2"], 3)], "PX") + lin("LA", [(uu, 1), (b, -1)]))
+          + lc + smul("LB" + sfx, [(PD["X2"], 3)], "PX") + lin("LA" + sfx, [(uu, 1), (b, -1)]))
     return [r1, r2]
 
 
-def prog_add_proj(px, py):
+def prog_add_proj(px, py, sfx=""):
     """T = (X : Y : xi W) -> T + (px, py) and the line through them at (PX, PY):
        TH = Y - py xi W, LAM = X - px xi W
        D = LAM^2, C = TH^2, K = W LAM, N = X LAM, J = TH LAM, V = W TH, YL = Y LAM
@@ -272,7 +281,7 @@ def prog_add_proj(px, py):
         return out
 
     th, lam = PA["TH"], PA["LAM"]
-    r1 = diff(th, "Y", py) + diff(lam, "X", px) + fixed_line_eval()
+    r1 = diff(th, "Y", py) + diff(lam, "X", px) + fixed_line_eval(sfx)
     r2 = (sq(PA["D"], [(lam, 1)]) + sq(PA["C"], [(th, 1)]) + mul(PA["K"], [("Z", 1)], [(lam, 1)])
           + mul(PA["N"], [("X", 1)], [(lam, 1)]) + mul(PA["J"], [(th, 1)], [(lam, 1)])
           + mul(PA["V"], [("Z", 1)], [(th, 1)]) + mul(PA["YL"], [("Y", 1)], [(lam, 1)]))
@@ -291,10 +300,10 @@ def prog_add_proj(px, py):
           for c in "xy"]
     y3 = [Lane(comp("Y", c), prod_terms([(j, 1)], [(n, 3), (d, -1)], c) + xi_times_c(vx, vy, c, -1)
                + prod_terms([(yl, -1)], [(d, 1)], c)) for c in "xy"]
-    la = [Lane(comp("LA", c), prod_terms([(th, 1)], [(px, 1)], c) + prod_terms([(lam, -1)], [(py, 1)], c))
+    la = [Lane(comp("LA" + sfx, c), prod_terms([(th, 1)], [(px, 1)], c) + prod_terms([(lam, -1)], [(py, 1)], c))
           for c in "xy"]
-    r3 = (x3 + y3 + mul("Z", [(k, 1)], [(d, 1)]) + smul("LC", [(lam, 1)], "PY") + smul("LB", [(th, -1)], "PX")
-          + la)
+    r3 = (x3 + y3 + mul("Z", [(k, 1)], [(d, 1)]) + smul("LC" + sfx, [(lam, 1)], "PY")
+          + smul("LB" + sfx, [(th, -1)], "PX") + la)
     return [r1, r2, r3]
 
 
@@ -827,7 +836,8 @@ def run_xround(xr, F, A, B):
 
 
 X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
-SCRATCH_CAP = {"FE": 96, "ML": 96}  # ML: slots C..L are free during the Miller loop
+# FE: the register file from register 2 on; ML: slots C..J during the Miller loop
+SCRATCH_CAP = {"FE": 48, "ML": 96}
 X_PROGRAMS = {  # name -> (program, scratch context)
     "PDBL": "ML", "PADD_POS": "ML", "PADD_NEG": "ML", "PADD_F1": "ML", "PADD_F2": "ML",
     "MDBL_1": "ML", "MDBL_2": "ML", "PDBL_1": "ML",
@@ -1006,6 +1016,7 @@ def validate_x(seed=2):
 SLOTS = ["F", "A", "B", "C", "D", "E", "G", "H", "I", "J", "K", "L"]   # enum S_F.. (bn256_pairing.h)
 F_BASE = 12 * len(SLOTS)
 SCR_BASE = {"FE": F_BASE + 2, "ML": 12 * SLOTS.index("C")}
+assert SCR_BASE["FE"] + SCRATCH_CAP["FE"] <= F_BASE + NREGS_RUNTIME
 
 
 def _pow_u_mul_instances(dst, sa):
@@ -1022,7 +1033,9 @@ INSTANCES = sorted(set(
                             ("K", "K", "H"), ("K", "K", "D"), ("J", "G", "D"), ("J", "J", "K"), ("K", "K", "C"),
                             ("K", "J", "L"), ("J", "J", "A"), ("F", "K", "J"), ("L", "F", "K"), ("A", "K", "L"),
                             ("F", "A", "B"), ("L", "A", "K"), ("F", "K", "L")]]
-    + _pow_u_mul_instances("C", "F") + _pow_u_mul_instances("D", "C") + _pow_u_mul_instances("E", "D")
+    # team_final_exp's exp-by-v chain (slots I <-> J, conjugate in K) and the a^u probe
+    + [("CYC_SQR_X", b) for b in [("J", "I"), ("J", "J"), ("I", "J"), ("I", "I")]]
+    + [("MUL12", b) for b in [("J", "J", "K"), ("J", "J", "I"), ("I", "I", "K"), ("I", "I", "J")]]
     + _pow_u_mul_instances("F", "A")
     + [("CYC_SQR_X", b) for b in [("K", "I"), ("J", "J"), ("K", "K"), ("F", "A")]]
     + [("SQR12", ("F", "F")), ("SQR12", ("F", "A")), ("LINE_PK", ("F", "F")), ("LINE_FIX", ("F", "F"))]
@@ -1069,8 +1082,10 @@ def bind(xr, binding, ctx):
             b["dst2"] = dst(L["dst2"])
         lanes.append(b)
     for L in lanes:
-        for v in [L["dst"], L.get("dst2", NONE)] + [d for d, _ in L["pre"]]:
-            assert v == NONE or v < F_BASE + NREGS, "index out of the team region"
+        srcs = [u for u, v in L["prod"] + L.get("prod2", [])] + [v for u, v in L["prod"] + L.get("prod2", [])]
+        srcs += [s_ for s_, _ in L["lin"] + L.get("lin2", [])] + [s_ for _, t in L["pre"] for s_, _ in t]
+        for v in [L["dst"], L.get("dst2", NONE)] + [d for d, _ in L["pre"]] + srcs:
+            assert v == NONE or v < F_BASE + NREGS_RUNTIME, "index out of the kernels' team region"
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
     return out
@@ -1143,8 +1158,8 @@ def emit_x(X, path):
         for i, (bx, off) in enumerate(rounds):
             # each round prefetches the next round's words (the last one: the caller's hint)
             nxt = f"XHint{{{rounds[i + 1][1]}, {rounds[i + 1][0].words()}}}" if i + 1 < len(rounds) else "h"
-            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {off}, {bx.np2}, {bx.nl2}, "
-                         f"{bx.kp}, {bx.kl1}, {bx.kl2}>(T, S, {nxt});")
+            calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
+                         f"{bx.kp}, {bx.kl1}, {bx.kl2}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
@@ -1168,7 +1183,9 @@ def emit(path):
     lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
              "// Lane-parallel team programs (see the generator for the encoding).",
              "#pragma once", "#include <stdint.h>", "namespace hg {",
-             f"static constexpr int kG2Regs = {NREGS};", f"static constexpr int kG2MaxSlots = {MAX_NSLOT};",
+             f"static constexpr int kG2Regs = {NREGS_RUNTIME};  // the kernels' register file",
+             f"static constexpr int kG2RegsAll = {NREGS};  // + the Jacobian cross-check programs' registers",
+             f"static constexpr int kG2MaxSlots = {MAX_NSLOT};",
              f"static constexpr int kG2MaxTerms = {MAX_TERMS};", f"static constexpr uint8_t kG2None = {NONE};",
              f"static constexpr int kOpSlotA = {SLOT_A};", f"static constexpr int kOpSlotB = {SLOT_B};"]
     for k, v in REG.items():
