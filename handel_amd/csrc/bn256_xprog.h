@@ -40,7 +40,7 @@ struct XHint {
   int off, w;  // table offset and per-lane stride of the round to prefetch (off < 0: none)
 };
 struct XStream;
-template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2>
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt);
 
 
@@ -181,7 +181,69 @@ HG_DEV void x_products(const Team& T, const uint32_t (&w)[W], int base, Acc& acc
     });
   }
 }
-template <int W, int NP, int NL, int KL>
+// Karatsuba products (the generator's per-job flag KS: jobs of 4+ products,
+// where the combination's ~55 instructions are repaid): with x = x0 +
+// 2^130 x1, y = y0 + 2^130 y1 (5-limb halves), a product is x0 y0, x1 y1 and
+// (x0 + x1)(y0 + y1) - x0 y0 - x1 y1: 75 mads instead of 100, plus 10 limb
+// additions. The three half-products accumulate over the whole job in their
+// own 9-column sets and combine into the job's columns once. Every column sum
+// and difference is taken mod 2^64; the combined columns equal the schoolbook
+// columns, which the generator keeps below 2^64 (and the half sums below 2^32,
+// check_xround), so the result is exact.
+struct KAcc {
+  uint64_t z0[9], z1[9], z2[9];
+};
+HG_DEV void kacc_mad_pinned(KAcc& k, const Fp& x, const Fp& y) {
+  uint32_t sx[5], sy[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    sx[i] = x.l[i] + x.l[i + 5];
+    sy[i] = y.l[i] + y.l[i + 5];
+  }
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      k.z0[i + j] += (uint64_t)x.l[i] * y.l[j];
+      asm("" : "+v"(k.z0[i + j]));
+      k.z2[i + j] += (uint64_t)x.l[i + 5] * y.l[j + 5];
+      asm("" : "+v"(k.z2[i + j]));
+      k.z1[i + j] += (uint64_t)sx[i] * sy[j];
+      asm("" : "+v"(k.z1[i + j]));
+    }
+}
+template <int W, int NP>
+HG_DEV void x_products_ks(const Team& T, const uint32_t (&w)[W], int base, Acc& acc) {
+  KAcc k;
+#pragma unroll
+  for (int c = 0; c < 9; c++) k.z0[c] = k.z1[c] = k.z2[c] = 0;
+  Fp a, b;
+  ld_fp_a8(a, x_at(T, x_off(w, base)));
+  ld_fp_a8(b, x_at(T, x_off(w, base + 1)));
+  x_for<NP>([&](auto p) {
+    Fp a2, b2;
+    if constexpr (p + 1 < NP) {
+      ld_fp_a8(a2, x_at(T, x_off(w, base + 2 * (p + 1))));
+      ld_fp_a8(b2, x_at(T, x_off(w, base + 2 * (p + 1) + 1)));
+    }
+    kacc_mad_pinned(k, a, b);
+#pragma unroll
+    for (int c = 0; c < 9; c++) asm volatile("" : "+v"(k.z0[c]), "+v"(k.z1[c]), "+v"(k.z2[c]));
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (p + 1 < NP) {
+      a = a2;
+      b = b2;
+    }
+  });
+#pragma unroll
+  for (int c = 0; c < 9; c++) {
+    acc.c[c] += k.z0[c];
+    acc.c[c + 10] += k.z2[c];
+    acc.c[c + 5] += k.z1[c] - (k.z0[c] + k.z2[c]);
+  }
+}
+
+template <int W, int NP, int NL, int KL, int KS>
 HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst) {
   Acc acc;
   acc_zero(acc);
@@ -192,7 +254,8 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 #pragma unroll
     for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] = val[l];
   }
-  x_products<W, NP>(T, w, base, acc);
+  if constexpr (KS) x_products_ks<W, NP>(T, w, base, acc);
+  else x_products<W, NP>(T, w, base, acc);
   dst = x_off(w, base + lbase + NL);
   if constexpr (NL > 0) acc_reduce_wide(r, acc);  // linear terms: result < 31p
   else acc_reduce(r, acc);                        // products only: < 2p, one subtraction
@@ -203,7 +266,7 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 // 0), job 2 (NP2 x (u, v), NL2 x term, dst2); padded to W dwords. Both jobs
 // read before either result is stored, so in-place programs are fine.
 // off: the round's table offset
-template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2>
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   if (S.off != off) x_fetch(T, S, XHint{off, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
@@ -222,11 +285,11 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   constexpr int jbase = NV * (1 + NT);
   Fp r;
   uint32_t dst;
-  x_job<W, NP, NL, KL1>(T, w, jbase, r, dst);
+  x_job<W, NP, NL, KL1, KS1>(T, w, jbase, r, dst);
   if constexpr (NP2 > 0 || NL2 > 0) {
     Fp r2;
     uint32_t dst2;
-    x_job<W, NP2, NL2, KL2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
+    x_job<W, NP2, NL2, KL2, KS2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
     team_sync();
     if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
     if (dst2 != 0xffffu) st_fp_a8(x_at(T, dst2), r2.l);

@@ -613,6 +613,7 @@ class XRound:
     def __init__(self, nv, nt, np_, nl, lanes, name, np2=0, nl2=0):
         self.nv, self.nt, self.np, self.nl, self.lanes, self.name = nv, nt, np_, nl, lanes, name
         self.np2, self.nl2 = np2, nl2
+        self.ks1 = self.ks2 = 0  # Karatsuba products per job (set by check_xround)
 
         def negk(terms):
             return sum(-k for _, k in terms if k < 0)
@@ -773,6 +774,14 @@ def check_xround(xr, order):
     jobs = [(L["prod"], L["lin"], xr.kl1, xr.nl) for L in xr.lanes]
     if xr.fused:
         jobs += [(L["prod2"], L["lin2"], xr.kl2, xr.nl2) for L in xr.lanes]
+    # Karatsuba per job (bn256_xprog.h x_products_ks): worth it from
+    # KARATSUBA_MIN products, valid while the 5-limb half sums stay 32-bit
+    def ks_ok(prods):
+        return len(prods) >= KARATSUBA_MIN and all(
+            max(lb[i] + lb[i + 5] for i in range(5)) < 1 << 32
+            for u, v in prods for lb in (src_bound(u)[1], src_bound(v)[1]))
+    xr.ks1 = int(all(ks_ok(L["prod"]) for L in xr.lanes))
+    xr.ks2 = int(xr.fused and all(ks_ok(L["prod2"]) for L in xr.lanes))
     for prod, lin, kl, nl in jobs:
         L = {"prod": prod, "lin": lin}
         if kl < 0:
@@ -836,6 +845,7 @@ def run_xround(xr, F, A, B):
 
 
 X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
+KARATSUBA_MIN = 4   # jobs of this many products use Karatsuba (when check_xround allows)
 # FE: the register file from register 2 on; ML: slots C..J during the Miller loop
 SCRATCH_CAP = {"FE": 48, "ML": 96}
 X_PROGRAMS = {  # name -> (program, scratch context)
@@ -1088,6 +1098,7 @@ def bind(xr, binding, ctx):
             assert v == NONE or v < F_BASE + NREGS_RUNTIME, "index out of the kernels' team region"
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
+    out.ks1, out.ks2 = xr.ks1, xr.ks2
     return out
 
 
@@ -1159,7 +1170,7 @@ def emit_x(X, path):
             # each round prefetches the next round's words (the last one: the caller's hint)
             nxt = f"XHint{{{rounds[i + 1][1]}, {rounds[i + 1][0].words()}}}" if i + 1 < len(rounds) else "h"
             calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
-                         f"{bx.kp}, {bx.kl1}, {bx.kl2}>(T, S, {off}, {nxt});")
+                         f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
