@@ -405,13 +405,16 @@ struct AggSched {
   int req_start[8];   // first entry of class c in order[]
   int nreq[7];
 };
-// Plan of every request (one thread each, grid-wide): counts, complement
-// decision, lanes; and its sort key for k_agg_order.
+// Plan of every request: counts, complement decision, lanes; and its sort
+// key for k_agg_order.
 static constexpr int kAggSub = 64;  // cost sub-buckets inside a lane class
+// One wave per request: the lanes scan the bitset's words side by side (the
+// loads coalesce and overlap instead of one thread's serial chain of them).
 __global__ __launch_bounds__(64) void k_agg_plan(const AggRequest* reqs, int n, const uint64_t* words,
                                                  const int32_t* codes, int nreg, int levels, AggPlan* plans,
                                                  int* keys) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
   if (r >= n) return;
   AggPlan p;
   if (codes[r] != HG_OK) {
@@ -423,13 +426,20 @@ __global__ __launch_bounds__(64) void k_agg_plan(const AggRequest* reqs, int n, 
   } else {
     const AggRequest q = reqs[r];
     uint32_t cnt = 0, nzs = 0, nzu = 0;
-    for (uint32_t wi = 0; wi < (q.bitlen + 63) / 64; wi++) cnt += __popcll(agg_word(q, words, wi));
-    for (uint32_t v = 0; v < agg_nrwords(q); v++) {
+    for (uint32_t wi = lane; wi < (q.bitlen + 63) / 64; wi += 64) cnt += __popcll(agg_word(q, words, wi));
+    for (uint32_t v = lane; v < agg_nrwords(q); v += 64) {
       nzs += nz_bytes(agg_rword(q, words, (int)v, false));
       nzu += nz_bytes(agg_rword(q, words, (int)v, true));
     }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      cnt += __shfl_xor(cnt, d);
+      nzs += __shfl_xor(nzs, d);
+      nzu += __shfl_xor(nzu, d);
+    }
     p = agg_plan(q, cnt, nzs, nzu, nreg, levels);
   }
+  if (lane != 0) return;
   plans[r] = p;
   int lg = 0;
   while ((1 << lg) < p.lanes) lg++;
@@ -834,7 +844,7 @@ void launch_aggregate(const PointG2* wsum, int nreg, const PointG2* blocks, cons
   AggPlan* plans = (AggPlan*)((uint8_t*)partial_ws + (size_t)n * sizeof(AggPartial));
   int* keys = (int*)(plans + n);
   AggSched* sched = (AggSched*)(keys + n);
-  k_agg_plan<<<nblk(n, 64), 64, 0, s>>>(reqs, n, words, codes, nreg, bi.levels, plans, keys);
+  k_agg_plan<<<n, 64, 0, s>>>(reqs, n, words, codes, nreg, bi.levels, plans, keys);
   k_agg_order<<<1, 1024, 0, s>>>(n, keys, order, sched);
   k_aggregate<<<n, 64, 0, s>>>(wsum, reqs, words, order, plans, sched, partial);
   k_agg_finish<<<nblk(n, 64), 64, 0, s>>>(blocks, bi, reqs, n, partial, out, codes);
