@@ -1,0 +1,54 @@
+// bn256_gt.h — data of the GT aggregate-verification path (bn256_gt.hip).
+#pragma once
+#include "bn256_kernels.h"
+
+namespace hg {
+
+// An Fp12 (GT) value in HBM, in the team slot layout: element e (10 limbs of
+// 26 bits, Montgomery form) at w[10 e], element order of bn256_team.h.
+struct Gt {
+  uint32_t w[120];
+};
+static constexpr int kGtChunk = 8;  // window-table values per fold chunk (one team)
+
+// per-request fold plan (k_gt_plan, k_gt_scan)
+struct GtReq {
+  int m;          // window-table terms of the folded mask
+  int chunks;     // ceil(m / kGtChunk)
+  int comp;       // folded over the complement inside the aligned block of level k
+  int k;
+  int term_off;   // first term in the batch's term list
+  int chunk_off;  // first chunk in the batch's chunk list
+};
+struct GtHdr {
+  int terms, chunks;
+};
+// level k >= 4 block j of the registry at blk[base[k] + j] (levels <= 3 are
+// window-table entries)
+struct GtBlockIndex {
+  int base[24];
+};
+// device workspaces of one fold launch
+struct GtWork {
+  GtReq* plan;
+  GtHdr* hdr;
+  uint32_t* terms;
+  int* chunk_req;
+  Gt* partial;
+  int chunk_grid;  // workgroups of k_gt_chunks (4 teams each)
+};
+
+// G_i = e(H, pk_i) for the n registry keys
+void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s);
+// win[256 w + s] = product of G_{8w + j} over the bits j of s (absent keys = 1)
+void launch_gt_windows(const Gt* key, int nreg, Gt* win, int nwin, hipStream_t s);
+// dst[j] = src[2j] * src[2j + 1] (entries `stride` apart; a missing odd entry = 1)
+void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s);
+// the fold of n requests: y[r] = conj(e(H, aggregate key of r)); codes: level
+// codes in, HG_ERR_EMPTY_AGG added for empty bitsets
+void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_t* codes, int nreg, int levels,
+                    const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, hipStream_t s);
+// FE(Miller(G2Base at -sig_r)) == y[r] for every request still HG_OK
+void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s);
+
+}  // namespace hg

@@ -1,0 +1,569 @@
+// bn256_gt.hip — aggregate verification in GT (the default path of
+// hg_verify_aggregate and its device / multisig variants).
+//
+// processing.go:342-368 verifies a multisignature as
+//     e(H, sum of the level's set keys) == e(sig, G2Base)
+// (bn256/go/bn256.go:82-94). H = hashedMessage(msg) is one point per Handel
+// run and the keys come from a fixed registry, so by bilinearity
+//     e(H, sum pk_i) = prod e(H, pk_i)
+// and every factor can be computed ONCE per (message, registry): the engine
+// keeps G_i = e(H, pk_i) and, as the G2 fold does for points, the products of
+// every subset of every aligned 8-key window (256 GT values per window) and of
+// every aligned power-of-two block. A request then costs
+//   * a GT fold: one Fp12 product per nonzero window byte of its bitset (or
+//     of the bitset's complement inside an aligned block: GT values are
+//     unitary, so the complement's inverse is a conjugate — no inversion,
+//     no affine conversion, nothing like k_agg_finish), and
+//   * ONE Miller loop (G2Base at -sig, lines from the table) plus the final
+//     exponentiation, compared with the folded value: the pk-side Miller loop
+//     (G2 doubling and addition programs, the pk lines) is gone.
+// The verdict is the reference's for every registry of keys in G2 (keys are
+// k * G2Base; the same parity scope as k_verify).
+//
+// Team layouts: k_gt_keys / k_verify_sig use the pairing team region of
+// k_verify (bn256_pairing.h); the fold kernels use the compact FOLD region of
+// the generator (slots F, A, B, registers ZERO and ONE, pre-pass scratch:
+// kFoldTeamElems elements), so several fold waves share a SIMD.
+#include <hip/hip_runtime.h>
+
+#include "bn256_agg.h"
+#include "bn256_gt.h"
+#include "bn256_pairing.h"
+
+namespace hg {
+static inline int nblk(int n, int b) { return (n + b - 1) / b; }
+
+static constexpr int kFoldWords = kFoldTeamElems * 10;
+static_assert(kFoldWords % 2 == 0, "8-byte aligned team regions");
+
+// ------------------------------------------------------------------ GT values in HBM <-> team slots
+// A GT value in HBM is the team slot layout: element e (10 limbs) at w[10 e].
+// Lane e < 12 moves element e; `conj` negates the odd powers of w on the way
+// in (the inverse of a unitary value). No sync: callers sync before reading.
+HG_DEV void gt_read(Fp& v, const Gt* g, const Team& T) {
+  const uint2* src = (const uint2*)__builtin_assume_aligned(g->w + 10 * T.e, 8);
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint2 x = src[i];
+    v.l[2 * i] = x.x;
+    v.l[2 * i + 1] = x.y;
+  }
+}
+HG_DEV void gt_put(const Team& T, int s, const Fp& v0, bool conj) {
+  Fp v = v0;
+  if (conj) {
+    Fp n;
+    fp_neg(n, v);
+    fp_sel(v, (T.k & 1) != 0, n, v);
+  }
+  if (T.active) st_fp_a8(slot(T, s) + T.e * 10, v.l);
+}
+HG_DEV void gt_load(const Team& T, int s, const Gt* g, bool conj = false) {
+  Fp v;
+  gt_read(v, g, T);
+  gt_put(T, s, v, conj);
+}
+HG_DEV void gt_one_value(Fp& v, const Team& T) {
+  Fp one;
+  fp_one(one);
+  fp_zero(v);
+  fp_sel(v, T.e == 1, one, v);  // element 1 = c0.y
+}
+// slot s = g (present) or 1
+HG_DEV void gt_load_or_one(const Team& T, int s, const Gt* g, bool present) {
+  Fp v, one;
+  gt_one_value(one, T);
+  if (present) gt_read(v, g, T);
+  fp_sel(v, present, v, one);
+  gt_put(T, s, v, false);
+}
+HG_DEV void gt_store(const Team& T, int s, Gt* g) {
+  Fp v;
+  ld_fp_a8(v, slot(T, s) + T.e * 10);
+  if (!T.active) return;
+  uint2* dst = (uint2*)__builtin_assume_aligned(g->w + 10 * T.e, 8);
+#pragma unroll
+  for (int i = 0; i < 5; i++) dst[i] = make_uint2(v.l[2 * i], v.l[2 * i + 1]);
+}
+// element-wise copy between team-region Fp12 values (LDS pointers)
+HG_DEV void lds_fp12_copy(const Team& T, uint32_t* dst, const uint32_t* src) {
+  Fp v;
+  ld_fp_a8(v, src + T.e * 10);
+  if (T.active) st_fp_a8(dst + T.e * 10, v.l);
+}
+
+// the FOLD region's constant registers (ZERO for padded products, ONE)
+HG_DEV void fold_regs_init(const Team& T) {
+  if (T.tl == 0) {
+    Fp z, o;
+    fp_zero(z);
+    fp_one(o);
+    st_fp_a8(T.base + (kFoldRegBase + 0) * 10, z.l);
+    st_fp_a8(T.base + (kFoldRegBase + 1) * 10, o.l);
+  }
+  team_sync();
+}
+using IMulF = XInst<XP_MUL12F, S_A, S_A, S_B>;  // A = A * B in the FOLD region
+HG_DEV void fold_mul(const Team& T, XStream& S) {
+  team_sync();
+  IMulF::run(T, S, xh<IMulF>());
+}
+
+// ------------------------------------------------------------------ per-(message, registry) tables
+// G_i = e(H, pk_i): the pairing team programs of k_verify with the G2Base
+// pairing switched off (unit lines), then the final exponentiation.
+template <int TEAMS>
+__global__ __launch_bounds__(64) void k_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* hpt,
+                                                Gt* out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
+  Team T = make_team(lds, kTeamWords);
+  uint32_t* F = team_regs(T);
+  const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
+  const bool valid = idx < n;
+  const PointG2& Q = reg[valid ? idx : n - 1];
+  CheckCtx C;
+  C.qx = Q.x;
+  C.qy = Q.y;
+  C.hx = hpt->x;
+  C.hy = hpt->y;
+  C.sx = hpt->x;
+  C.sy = hpt->y;
+  C.use_q = Q.inf == 0;
+  C.use_s = false;
+  if (!C.use_q) {  // e(H, infinity) = 1: unit lines on a well-defined doubling chain
+    const Fp2 gx = HG_G2X, gy = HG_G2Y;
+    C.qx = gx;
+    C.qy = gy;
+  }
+  XStream S = x_stream();
+  team_miller_check(T, F, C, tab, false, S, final_exp_hint());
+  team_final_exp(T, F, S);
+  if (valid) gt_store(T, S_F, out + idx);
+}
+
+// Window subset products, first pass: for each window w and half h (keys
+// 8w + 4h .. 8w + 4h + 3) the 16 products of the half's subsets, by the
+// recurrence P(s) = P(s without its lowest bit) * G(lowest bit), kept in LDS;
+// entries s (h = 0) and s << 4 (h = 1) of the window's table. Absent keys
+// (past the registry) are 1.
+__global__ __launch_bounds__(64) void k_gt_nib(const Gt* key, int nreg, int nwin, Gt* win) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
+  __shared__ __attribute__((aligned(16))) uint32_t dp[4][16 * kFp12Words];
+  Team T = make_team(lds, kFoldWords);
+  fold_regs_init(T);
+  const int team = (threadIdx.x & 63) >> 4;
+  const int task = blockIdx.x * 4 + team;
+  const bool valid = task < 2 * nwin;
+  const int w = valid ? task >> 1 : 0, h = task & 1;
+  uint32_t* D = dp[team];
+  XStream S = x_stream();
+  Fp one;
+  gt_one_value(one, T);
+  if (T.active) st_fp_a8(D + T.e * 10, one.l);  // P(empty) = 1
+#pragma unroll 1
+  for (int s = 1; s < 16; s++) {
+    const int lo = s & -s, rest = s ^ lo;
+    if (rest == 0) {
+      const int j = 31 - __clz(lo);
+      const int kidx = 8 * w + 4 * h + j;
+      gt_load_or_one(T, S_A, key + (kidx < nreg ? kidx : 0), kidx < nreg);
+    } else {
+      lds_fp12_copy(T, slot(T, S_A), D + rest * kFp12Words);
+      lds_fp12_copy(T, slot(T, S_B), D + lo * kFp12Words);
+      fold_mul(T, S);
+    }
+    team_sync();
+    lds_fp12_copy(T, D + s * kFp12Words, slot(T, S_A));
+  }
+  team_sync();
+  if (!valid) return;
+  Gt* tw = win + (size_t)w * 256;
+#pragma unroll 1
+  for (int s = (h ? 1 : 0); s < 16; s++) {
+    Fp v;
+    ld_fp_a8(v, D + s * kFp12Words + T.e * 10);
+    if (!T.active) continue;
+    uint2* dst = (uint2*)__builtin_assume_aligned(tw[h ? s << 4 : s].w + 10 * T.e, 8);
+#pragma unroll
+    for (int i = 0; i < 5; i++) dst[i] = make_uint2(v.l[2 * i], v.l[2 * i + 1]);
+  }
+}
+
+// Second pass: entry (hi << 4) | lo = entry(lo) * entry(hi << 4) for hi, lo
+// != 0; one team per (window, hi), 15 products.
+__global__ __launch_bounds__(64) void k_gt_cross(int nwin, Gt* win) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
+  Team T = make_team(lds, kFoldWords);
+  fold_regs_init(T);
+  const int task = blockIdx.x * 4 + ((threadIdx.x & 63) >> 4);
+  const bool valid = task < 15 * nwin;
+  const int w = valid ? task / 15 : 0, hi = valid ? task % 15 + 1 : 1;
+  Gt* tw = win + (size_t)w * 256;
+  XStream S = x_stream();
+#pragma unroll 1
+  for (int lo = 1; lo < 16; lo++) {
+    gt_load(T, S_A, tw + lo);
+    gt_load(T, S_B, tw + (hi << 4));
+    fold_mul(T, S);
+    team_sync();
+    if (valid) gt_store(T, S_A, tw + ((hi << 4) | lo));
+  }
+}
+
+// Block products, one level: dst[j] = src[2j] * src[2j + 1] (the last block of
+// a level may be clipped: src[2j + 1] absent -> 1). src entries `stride` apart.
+__global__ __launch_bounds__(64) void k_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
+  Team T = make_team(lds, kFoldWords);
+  fold_regs_init(T);
+  const int j = blockIdx.x * 4 + ((threadIdx.x & 63) >> 4);
+  const bool valid = j < ndst;
+  const int a = valid ? 2 * j : 0;
+  XStream S = x_stream();
+  gt_load(T, S_A, src + (size_t)a * stride);
+  gt_load_or_one(T, S_B, src + (size_t)(a + 1 < nsrc ? a + 1 : a) * stride, a + 1 < nsrc);
+  fold_mul(T, S);
+  team_sync();
+  if (valid) gt_store(T, S_A, dst + j);
+}
+
+// ------------------------------------------------------------------ the fold of a batch
+// Plan (one wave per request): set count, nonzero window bytes of the bitset
+// and of its complement, the complement decision (agg_plan, as the G2 fold),
+// the request's term count m and chunk count; an empty bitset is the
+// reference's nil-aggregate panic (HG_ERR_EMPTY_AGG).
+__global__ __launch_bounds__(64) void k_gt_plan(const AggRequest* reqs, int n, const uint64_t* words, int32_t* codes,
+                                                int nreg, int levels, GtReq* plan) {
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (r >= n) return;
+  GtReq g;
+  g.m = g.chunks = g.comp = g.k = 0;
+  if (codes[r] == HG_OK) {
+    const AggRequest q = reqs[r];
+    uint32_t cnt = 0, nzs = 0, nzu = 0;
+    for (uint32_t wi = lane; wi < (q.bitlen + 63) / 64; wi += 64) cnt += __popcll(agg_word(q, words, wi));
+    for (uint32_t v = lane; v < agg_nrwords(q); v += 64) {
+      nzs += nz_bytes(agg_rword(q, words, (int)v, false));
+      nzu += nz_bytes(agg_rword(q, words, (int)v, true));
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      cnt += __shfl_xor(cnt, d);
+      nzs += __shfl_xor(nzs, d);
+      nzu += __shfl_xor(nzu, d);
+    }
+    const AggPlan p = agg_plan(q, cnt, nzs, nzu, nreg, levels);
+    if (cnt == 0) {
+      if (lane == 0) codes[r] = HG_ERR_EMPTY_AGG;
+    } else {
+      g.m = (int)p.m;
+      g.chunks = (g.m + kGtChunk - 1) / kGtChunk;
+      g.comp = p.comp ? 1 : 0;
+      g.k = p.k;
+    }
+  }
+  if (lane == 0) plan[r] = g;
+}
+
+// Exclusive prefix sums of the term and chunk counts (one block), totals in hdr.
+__global__ __launch_bounds__(1024) void k_gt_scan(int n, GtReq* plan, GtHdr* hdr) {
+  __shared__ int sm[1024], sc[1024];
+  __shared__ int carry_m, carry_c;
+  const int t = threadIdx.x;
+  if (t == 0) carry_m = carry_c = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + t;
+    const int m = i < n ? plan[i].m : 0, c = i < n ? plan[i].chunks : 0;
+    sm[t] = m;
+    sc[t] = c;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      const int xm = t >= d ? sm[t - d] : 0, xc = t >= d ? sc[t - d] : 0;
+      __syncthreads();
+      sm[t] += xm;
+      sc[t] += xc;
+      __syncthreads();
+    }
+    if (i < n) {
+      plan[i].term_off = carry_m + sm[t] - m;
+      plan[i].chunk_off = carry_c + sc[t] - c;
+    }
+    __syncthreads();
+    if (t == 1023) {
+      carry_m += sm[t];
+      carry_c += sc[t];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    hdr->terms = carry_m;
+    hdr->chunks = carry_c;
+  }
+}
+
+// Terms (one wave per request): the window-table index 256 w + byte of every
+// nonzero byte of the folded mask in registry-aligned windows, in order; and
+// the owner of each of the request's chunks.
+__global__ __launch_bounds__(64) void k_gt_terms(const AggRequest* reqs, int n, const uint64_t* words,
+                                                 const int32_t* codes, const GtReq* plan, uint32_t* terms,
+                                                 int* chunk_req) {
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (r >= n || codes[r] != HG_OK) return;
+  const GtReq g = plan[r];
+  if (g.m == 0) return;
+  const AggRequest q = reqs[r];
+  const uint32_t nrw = agg_nrwords(q);
+  const uint32_t win0 = q.offset >> 3;
+  uint32_t at = g.term_off;
+  for (uint32_t v0 = 0; v0 < nrw; v0 += 64) {
+    const uint32_t v = v0 + lane;
+    const uint64_t mb = v < nrw ? agg_rword(q, words, (int)v, g.comp != 0) : 0;
+    const uint32_t pc = nz_bytes(mb);
+    uint32_t inc = pc;  // inclusive prefix over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t x = __shfl_up(inc, d);
+      if (lane >= d) inc += x;
+    }
+    uint32_t pos = at + inc - pc;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t byte = (uint32_t)(mb >> (8 * j)) & 255u;
+      if (byte) terms[pos++] = (win0 + 8 * v + j) * 256u + byte;
+    }
+    at += __shfl(inc, 63);
+  }
+  for (int c = lane; c < g.chunks; c += 64) chunk_req[g.chunk_off + c] = r;
+}
+
+// Chunks: each team multiplies the (at most kGtChunk) window-table values of
+// one chunk into a partial product. A fixed grid walks the chunk list (the
+// count is on the device); every wave runs to the same, wave-uniform bound.
+// The next term is fetched from HBM into registers while the current product
+// runs.
+__global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const uint32_t* terms, const int* chunk_req,
+                                                  const GtReq* plan, const GtHdr* hdr, Gt* partial) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
+  Team T = make_team(lds, kFoldWords);
+  fold_regs_init(T);
+  const int team = (threadIdx.x & 63) >> 4;
+  const int total = hdr->chunks;
+  XStream S = x_stream();
+  for (int base = blockIdx.x * 4; base < total; base += gridDim.x * 4) {  // wave-uniform
+    const int c = base + team;
+    const bool valid = c < total;
+    int first = 0, cnt = 0;
+    if (valid) {
+      const GtReq g = plan[chunk_req[c]];
+      first = g.term_off + (c - g.chunk_off) * kGtChunk;
+      cnt = min(kGtChunk, g.term_off + g.m - first);
+    }
+    int maxc = cnt;
+#pragma unroll
+    for (int d = 16; d < 64; d <<= 1) maxc = max(maxc, __shfl_xor(maxc, d));
+    gt_load_or_one(T, S_A, win + (valid ? terms[first] : 0), valid);
+    Fp nxt;
+    fp_zero(nxt);
+    if (1 < cnt) gt_read(nxt, win + terms[first + 1], T);
+#pragma unroll 1
+    for (int i = 1; i < maxc; i++) {
+      Fp one, v;
+      gt_one_value(one, T);
+      fp_sel(v, i < cnt, nxt, one);
+      gt_put(T, S_B, v, false);
+      if (i + 1 < cnt) gt_read(nxt, win + terms[first + i + 1], T);  // in flight across the product
+      fold_mul(T, S);
+    }
+    team_sync();
+    if (valid) gt_store(T, S_A, partial + c);
+    team_sync();
+  }
+}
+
+// Combine (one wave per request): the 4 teams multiply every 4th partial, a
+// 2-level tree joins them, then the target of the pairing check:
+//   Y = conj(agg) = conj(prod)             (plain fold)
+//   Y = conj(block * conj(prod)) = conj(block) * prod   (complemented fold)
+__global__ __launch_bounds__(64) void k_gt_combine(const AggRequest* reqs, int n, const int32_t* codes,
+                                                   const GtReq* plan, const Gt* partial, const Gt* win,
+                                                   const Gt* blk, GtBlockIndex bi, Gt* y) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
+  const int r = blockIdx.x;
+  if (r >= n || codes[r] != HG_OK) return;  // one request per wave: uniform
+  Team T = make_team(lds, kFoldWords);
+  fold_regs_init(T);
+  const int team = (threadIdx.x & 63) >> 4;
+  const GtReq g = plan[r];
+  XStream S = x_stream();
+  const int rounds = (g.chunks + 3) / 4;
+  gt_load_or_one(T, S_A, partial + (team < g.chunks ? g.chunk_off + team : 0), team < g.chunks);
+#pragma unroll 1
+  for (int i = 1; i < rounds; i++) {
+    const int c = team + 4 * i;
+    gt_load_or_one(T, S_B, partial + (c < g.chunks ? g.chunk_off + c : 0), c < g.chunks);
+    fold_mul(T, S);
+  }
+  if (g.chunks > 1) {
+    for (int d = 1; d < 4; d <<= 1) {
+      team_sync();
+      lds_fp12_copy(T, slot(T, S_B), lds + (team ^ d) * kFoldWords + S_A * kFp12Words);
+      fold_mul(T, S);
+    }
+  }
+  team_sync();
+  if (g.comp) {
+    const AggRequest q = reqs[r];
+    const Gt* B;
+    if (g.k <= 3) {  // a block inside one window: that window's subset entry
+      const uint32_t mask = ((1u << (1u << g.k)) - 1u) << (q.offset & 7u);
+      B = win + (size_t)(q.offset >> 3) * 256 + (mask & 255u);
+    } else {
+      B = blk + bi.base[g.k] + (q.offset >> g.k);
+    }
+    gt_load(T, S_B, B, true);
+    fold_mul(T, S);
+  } else {
+    Fp v;
+    ld_fp_a8(v, slot(T, S_A) + T.e * 10);
+    team_sync();
+    gt_put(T, S_A, v, true);
+  }
+  team_sync();
+  if (team == 0) gt_store(T, S_A, y + r);
+}
+
+// ------------------------------------------------------------------ the pairing check
+// f = Miller(G2Base at -sig) (x/crypto optate.go miller with the G2Base lines
+// from the table): per doubling f^2 with the line's evaluation at -sig beside
+// it (SDBL), then f * line; an addition's line is evaluated beside the
+// previous product (LFEV). Lanes 12..15 evaluate, lanes 0..11 run the Fp12
+// job, so the evaluation is free.
+using ISdbl = XInst<XP_SDBL, S_F, S_F>;
+using ILfev = XInst<XP_LFEV, S_F, S_F>;
+using IFeval = XInst<XP_FEVAL>;
+using ILfix = XInst<XP_LINE_FIX, S_F, S_F>;
+
+// FBX, FCY of line s (the evaluation's inputs) / FA of line s
+HG_DEV void load_line_bc(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
+  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
+  if (T.tl >= 2 && T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
+  team_sync();
+}
+HG_DEV void load_line_a(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
+  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
+  if (T.tl < 2) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
+  team_sync();
+}
+HG_DEV void sig_unit_fix(const Team& T, uint32_t* F, bool use_s) {
+  team_sync();
+  unit_line_regs(T, F, !use_s, R_FA_x, R_FB_x, R_FC_x);
+}
+
+HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& sy, bool use_s,
+                            const LineCoef* tab, XStream& S, XHint after) {
+  const int8_t naf[kNafLen] = HG_NAF;
+  t12_set_one(T, S_F);
+  if (T.tl == 0) {
+    Fp zero, one, nsy;
+    fp_zero(zero);
+    fp_one(one);
+    fp_neg(nsy, sy);
+    st_fp(F + R_ZERO * 10, zero);
+    st_fp(F + R_ONE * 10, one);
+    st_fp(F + R_SX * 10, sx);
+    st_fp(F + R_NSY * 10, nsy);
+  }
+  team_sync();
+  int s = 0;
+  for (int i = kNafLen - 1; i > 0; i--) {
+    const int d = naf[i - 1];
+    load_line_bc(T, F, tab, s);
+    load_line_a(T, F, tab, s);
+    // f^2 (f = 1 on the first digit) beside line s evaluated at -sig
+    ISdbl::run(T, S, d != 0 ? xh<ILfev>() : xh<ILfix>());
+    sig_unit_fix(T, F, use_s);
+    const XHint after_digit = i > 1 ? xh<ISdbl>() : xh<IFeval>();
+    if (d != 0) {
+      load_line_bc(T, F, tab, s + 1);  // read by the evaluation beside f * line s
+      ILfev::run(T, S, xh<ILfix>());
+      load_line_a(T, F, tab, s + 1);
+      sig_unit_fix(T, F, use_s);
+      ILfix::run(T, S, after_digit);
+      s += 2;
+    } else {
+      ILfix::run(T, S, after_digit);
+      s += 1;
+    }
+  }
+  // the two Frobenius lines
+  load_line_bc(T, F, tab, s);
+  load_line_a(T, F, tab, s);
+  IFeval::run(T, S, xh<ILfev>());
+  sig_unit_fix(T, F, use_s);
+  load_line_bc(T, F, tab, s + 1);
+  ILfev::run(T, S, xh<ILfix>());
+  load_line_a(T, F, tab, s + 1);
+  sig_unit_fix(T, F, use_s);
+  ILfix::run(T, S, after);
+}
+
+// true (team-uniform) when slots a and b hold the same value (both canonical)
+HG_DEV bool t12_equal(const Team& T, int a, int b) {
+  Fp u, v;
+  ld_fp_a8(u, slot(T, a) + T.e * 10);
+  ld_fp_a8(v, slot(T, b) + T.e * 10);
+  const bool ok = fp_eq(u, v) || !T.active;
+  const uint64_t bal = __ballot(ok);
+  const int team_shift = (threadIdx.x & 63) & ~15;
+  return ((bal >> team_shift) & 0xffffull) == 0xffffull;
+}
+
+// FE(Miller(G2Base at -sig)) == Y_r  <=>  e(H, agg) * e(-sig, G2Base) == 1
+template <int TEAMS>
+__global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y,
+                                                   int32_t* codes) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
+  Team T = make_team(lds, kTeamWords);
+  uint32_t* F = team_regs(T);
+  const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
+  const bool valid = idx < n;
+  const int ci = valid ? idx : n - 1;
+  const PointG1 sg = sigs[ci];
+  XStream S = x_stream();
+  team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, final_exp_hint());
+  team_final_exp(T, F, S);
+  gt_load(T, S_A, y + ci);
+  team_sync();
+  const bool ok = t12_equal(T, S_F, S_A);
+  if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
+}
+
+// ------------------------------------------------------------------ launchers
+void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s) {
+  if (n > 0) k_gt_keys<4><<<nblk(n, 4), 64, 0, s>>>(reg, n, tab, h, out);
+}
+void launch_gt_windows(const Gt* key, int nreg, Gt* win, int nwin, hipStream_t s) {
+  if (nwin <= 0) return;
+  k_gt_nib<<<nblk(2 * nwin, 4), 64, 0, s>>>(key, nreg, nwin, win);
+  k_gt_cross<<<nblk(15 * nwin, 4), 64, 0, s>>>(nwin, win);
+}
+void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s) {
+  if (ndst > 0) k_gt_blocks<<<nblk(ndst, 4), 64, 0, s>>>(src, stride, nsrc, dst, ndst);
+}
+void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_t* codes, int nreg, int levels,
+                    const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, hipStream_t s) {
+  if (n <= 0) return;
+  k_gt_plan<<<n, 64, 0, s>>>(reqs, n, words, codes, nreg, levels, w.plan);
+  k_gt_scan<<<1, 1024, 0, s>>>(n, w.plan, w.hdr);
+  k_gt_terms<<<n, 64, 0, s>>>(reqs, n, words, codes, w.plan, w.terms, w.chunk_req);
+  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, w.terms, w.chunk_req, w.plan, w.hdr, w.partial);
+  k_gt_combine<<<n, 64, 0, s>>>(reqs, n, codes, w.plan, w.partial, win, blk, bi, y);
+}
+void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
+  if (n > 0) k_verify_sig<4><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, y, codes);
+}
+
+}  // namespace hg

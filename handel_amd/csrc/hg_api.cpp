@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "bn256_gt.h"
 #include "bn256_kernels.h"
 
 using namespace hg;
@@ -173,6 +174,18 @@ struct hg_ctx {
   DevBuf<int> order;       // aggregation schedule (k_agg_order)
   DevBuf<uint8_t> agg_ws;  // per-request fold results (k_aggregate -> k_agg_finish)
   DevBuf<uint64_t> words;
+  // GT path of aggregate verification (bn256_gt.hip): e(H, pk_i), window
+  // subset products and block products, valid for the current message and
+  // registry (rebuilt by the first aggregate submission after either changes)
+  bool gt_ready = false;
+  DevBuf<Gt> gt_key, gt_win, gt_blk;
+  GtBlockIndex gt_bi{};
+  // GT fold workspaces
+  DevBuf<GtReq> gt_plan;
+  DevBuf<GtHdr> gt_hdr;
+  DevBuf<uint32_t> gt_terms;
+  DevBuf<int> gt_chunk_req;
+  DevBuf<Gt> gt_partial, gt_y;
   // submission order across streams: the event recorded after the last
   // submission and the stream it ran on (the workspaces above are shared)
   hipEvent_t last_ev = nullptr;
@@ -270,6 +283,16 @@ static void release_all(hg_ctx* c) {
   c->order.release();
   c->agg_ws.release();
   c->words.release();
+  c->gt_key.release();
+  c->gt_win.release();
+  c->gt_blk.release();
+  c->gt_plan.release();
+  c->gt_hdr.release();
+  c->gt_terms.release();
+  c->gt_chunk_req.release();
+  c->gt_partial.release();
+  c->gt_y.release();
+  c->gt_ready = false;
   for (auto& ph : c->events) {
     for (auto& pr : ph) {
       (void)hipEventDestroy(pr.first);
@@ -298,6 +321,7 @@ static int set_message_locked(hg_ctx* c, const uint8_t* msg, size_t len) {
   sha256(msg, len, d);
   uint32_t k[8];
   c->has_msg = false;
+  c->gt_ready = false;  // the GT tables are e(H, .) of the previous message
   c->msg.assign(msg, msg + len);
   c->hash_eof = !hash_scalar(d, k);
   if (c->hash_eof) {
@@ -360,6 +384,64 @@ static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector
   }
 }
 
+// Which fold verifies aggregate requests: the GT path (bn256_gt.hip, default)
+// or the G2 point fold + k_verify (HG_AGG_PATH=g2, kept for A/B runs).
+static bool gt_path_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("HG_AGG_PATH");
+    return !(e && strcmp(e, "g2") == 0);
+  }();
+  return on;
+}
+
+// e(H, pk_i), the window subset products and the block products of levels
+// k >= 4 (levels <= 3 are window entries) for the current message and
+// registry, on stream s (inside a submission).
+static int build_gt_locked(hg_ctx* c, hipStream_t s) {
+  const int n = (int)c->nreg;
+  const int nwin = (n + 7) / 8;
+  HG_CHECK(c, c->gt_key.ensure(n));
+  HG_CHECK(c, c->gt_win.ensure((size_t)nwin * 256));
+  int cnt[24] = {0};
+  int total = 0;
+  for (int k = 4; k <= c->block_levels && k < 24; k++) {
+    cnt[k] = (int)(((size_t)n + ((size_t)1 << k) - 1) >> k);
+    c->gt_bi.base[k] = total;
+    total += cnt[k];
+  }
+  if (total) HG_CHECK(c, c->gt_blk.ensure(total));
+  launch_gt_keys(c->reg.p, n, c->d_lines, c->d_h, c->gt_key.p, s);
+  launch_gt_windows(c->gt_key.p, n, c->gt_win.p, nwin, s);
+  for (int k = 4; k <= c->block_levels && k < 24; k++) {
+    if (k == 4) launch_gt_blocks(c->gt_win.p + 255, 256, nwin, c->gt_blk.p + c->gt_bi.base[4], cnt[4], s);
+    else launch_gt_blocks(c->gt_blk.p + c->gt_bi.base[k - 1], 1, cnt[k - 1], c->gt_blk.p + c->gt_bi.base[k], cnt[k], s);
+  }
+  int rc = check_launch(c);
+  if (rc) return rc;
+  c->gt_ready = true;
+  return HG_OK;
+}
+
+// GT fold workspaces for n requests: a request's folded mask has at most
+// 8 * (registry-aligned words) nonzero window bytes
+static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
+  const size_t mmax = 8 * ((c->nreg + 7 + 63) / 64 + 1);
+  const size_t cmax = (mmax + kGtChunk - 1) / kGtChunk;
+  HG_CHECK(c, c->gt_plan.ensure(n));
+  HG_CHECK(c, c->gt_hdr.ensure(1));
+  HG_CHECK(c, c->gt_terms.ensure(n * mmax));
+  HG_CHECK(c, c->gt_chunk_req.ensure(n * cmax));
+  HG_CHECK(c, c->gt_partial.ensure(n * cmax));
+  HG_CHECK(c, c->gt_y.ensure(n));
+  w.plan = c->gt_plan.p;
+  w.hdr = c->gt_hdr.p;
+  w.terms = c->gt_terms.p;
+  w.chunk_req = c->gt_chunk_req.p;
+  w.partial = c->gt_partial.p;
+  w.chunk_grid = 2048;
+  return HG_OK;
+}
+
 // The Combine fold and (verify) the pairing check of n requests, device
 // pointers, on stream s; d_lvl holds the level codes and is updated in place.
 static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
@@ -369,19 +451,38 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     c->err = "hg_set_message was not called";
     return HG_ERR_ARG;
   }
-  HG_CHECK(c, c->checks.ensure(n));
-  HG_CHECK(c, c->order.ensure(n));
-  HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
+  // GT path: the verdict needs no aggregate key in G2; the G2 fold still runs
+  // when the caller wants the aggregate keys' marshals
+  const bool use_gt = verify && gt_path_enabled() && !c->hash_eof && c->nreg > 0;
+  const bool g2_fold = !use_gt || d_agg;
+  GtWork gw{};
+  if (use_gt) {
+    int rc = ensure_gt_fold(c, n, gw);
+    if (rc) return rc;
+  }
+  if (g2_fold) {
+    HG_CHECK(c, c->checks.ensure(n));
+    HG_CHECK(c, c->order.ensure(n));
+    HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
+  }
   if (d_agg) HG_CHECK(c, c->pts2.ensure(n));
   if (verify) {
     HG_CHECK(c, c->pts1.ensure(n));
     HG_CHECK(c, c->codes_b.ensure(n));
   }
   HG_CHECK(c, begin(c, s));
+  if (use_gt && !c->gt_ready) {
+    int rc = build_gt_locked(c, s);
+    if (rc) return rc;
+  }
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
   PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
-  launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
-                   d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
+  if (g2_fold)
+    launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
+                     d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
+  if (use_gt)
+    launch_gt_fold(d_reqs, (int)n, d_words, d_lvl, (int)c->nreg, c->block_levels, c->gt_win.p, c->gt_blk.p,
+                   c->gt_bi, gw, c->gt_y.p, s);
   fold.stop();
   if (d_agg) {
     launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);
@@ -390,7 +491,11 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   if (verify) {
     launch_decode_g1(d_sigs, (int)n, c->flavor, c->pts1.p, c->codes_b.p, s);
     k_agg_codes<<<nb(n), 256, 0, s>>>(c->codes_b.p, d_lvl, c->hash_eof ? 1 : 0, (int)n, d_codes);
-    if (!c->hash_eof) {
+    if (use_gt) {
+      PhaseTimer t(c, HG_PHASE_VERIFY, s);
+      launch_verify_sig(c->pts1.p, (int)n, c->d_lines, c->gt_y.p, d_codes, s);
+      t.stop();
+    } else if (!c->hash_eof) {
       launch_sig_into_checks(c->pts1.p, (int)n, c->checks.p, s);
       timed_verify(c, c->checks.p, (int)n, d_codes, s);
     }
@@ -570,6 +675,7 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   // leaves it empty (every aggregate request then fails its range check)
   c->nreg = 0;
   c->block_levels = 0;
+  c->gt_ready = false;
   HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   HG_CHECK(c, c->reg.ensure(n));

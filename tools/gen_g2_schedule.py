@@ -479,6 +479,14 @@ PROGRAMS = {
     "PADD_F1": prog_add_proj("P1X", "P1Y"),
     "PADD_F2": prog_add_proj("P2X", "QY"),
 }
+# Sig-only Miller loop (bn256_gt.hip k_verify_sig): the G2Base line at -sig is
+# evaluated on lanes 12..15 beside f^2 (SDBL) or beside f * the previous line
+# (LFEV), rounds whose Fp12 jobs leave those lanes idle anyway; FEVAL alone.
+PROGRAMS["FEVAL"] = [fixed_line_eval()]
+PROGRAMS["SDBL"] = [prog_sqr12()[0] + fixed_line_eval()]
+PROGRAMS["LFEV"] = [prog_line("FA", "FB", "FC")[0] + fixed_line_eval()]
+# Fp12 product in the compact GT-fold team layout (context FOLD below)
+PROGRAMS["MUL12F"] = prog_mul12()
 # programs also emitted in the single-phase table format (bn256_g2sched.h)
 LEGACY = ("DBL", "ADD_POS", "ADD_NEG", "ADD_F1", "ADD_F2", "CYC_SQR", "SQR12")
 
@@ -847,7 +855,9 @@ def run_xround(xr, F, A, B):
 X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
 KARATSUBA_MIN = 4   # jobs of this many products use Karatsuba (when check_xround allows)
 # FE: the register file from register 2 on; ML: slots C..J during the Miller loop
-SCRATCH_CAP = {"FE": 48, "ML": 96}
+# FOLD: the GT fold kernels' compact team region (bn256_gt.hip): slots F, A, B,
+# then registers ZERO and ONE, then the pre-pass scratch
+SCRATCH_CAP = {"FE": 48, "ML": 96, "FOLD": 48}
 X_PROGRAMS = {  # name -> (program, scratch context)
     "PDBL": "ML", "PADD_POS": "ML", "PADD_NEG": "ML", "PADD_F1": "ML", "PADD_F2": "ML",
     "MDBL_1": "ML", "MDBL_2": "ML", "PDBL_1": "ML",
@@ -855,6 +865,7 @@ X_PROGRAMS = {  # name -> (program, scratch context)
     "PADD_NEG_3": "ML", "PADD_F1_1": "ML", "MADD_F1_2": "ML", "PADD_F1_3": "ML", "PADD_F2_1": "ML",
     "MADD_F2_2": "ML", "PADD_F2_3": "ML",
     "SQR12": "ML", "LINE_PK": "ML", "LINE_FIX": "ML", "CYC_SQR": "FE", "MUL12": "FE", "CYC_SQR_X": "FE",
+    "FEVAL": "ML", "SDBL": "ML", "LFEV": "ML", "MUL12F": "FOLD",
 }
 
 
@@ -998,6 +1009,24 @@ def validate_x(seed=2):
             run_xprogram(X[f"PADD_{v}_3"], G)
             assert unfl(d2) == O._mul_line(f0, *fix), "xMADD fixed line"
             check_proj(G, r_new, (a, b, c), "x" + prog + " split")
+        # sig-only Miller rounds: f^2 / f * line with the next line's evaluation beside
+        G = dict(F)
+        sq = run_xprogram(X["SDBL"], G, flat0)
+        assert unfl(sq) == O.f12_sqr(f0), "xSDBL square"
+        assert (getf(G, "FB"), getf(G, "FC")) == fix[1:], "xSDBL line evaluation"
+        G = dict(F)
+        put(G, "FB", fix[1])
+        put(G, "FC", fix[2])
+        nbx, ncy = (rng.randrange(P), rng.randrange(P)), (rng.randrange(P), rng.randrange(P))
+        put(G, "FBX", nbx)
+        put(G, "FCY", ncy)
+        d2 = run_xprogram(X["LFEV"], G, flat0)
+        assert unfl(d2) == O._mul_line(f0, *fix), "xLFEV line"
+        assert (getf(G, "FB"), getf(G, "FC")) == (O.f2_mul(nbx, (0, F[REG["SX"]])),
+                                                  O.f2_mul(ncy, (0, F[REG["NSY"]]))), "xLFEV evaluation"
+        G = dict(F)
+        run_xprogram(X["FEVAL"], G)
+        assert (getf(G, "FB"), getf(G, "FC")) == fix[1:], "xFEVAL"
         f = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
         g = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
         flat = lambda v: [z for pair in v for z in pair]  # noqa: E731
@@ -1008,6 +1037,7 @@ def validate_x(seed=2):
         assert unflat(run_xprogram(X["CYC_SQR"], dict(F), flat(cyc))) == O.f12_sqr(cyc), "xCYC_SQR"
         assert unflat(run_xprogram(X["CYC_SQR_X"], dict(F), flat(cyc))) == O.f12_sqr(cyc), "xCYC_SQR_X"
         assert unflat(run_xprogram(X["MUL12"], dict(F), flat(f), flat(g))) == O.f12_mul(f, g), "xMUL12"
+        assert unflat(run_xprogram(X["MUL12F"], dict(F), flat(f), flat(g))) == O.f12_mul(f, g), "xMUL12F"
         G = dict(F)
         la, lb, lc = [(rng.randrange(P), rng.randrange(P)) for _ in range(3)]
         for regs in (("LA", "LB", "LC", "LINE_PK"), ("FA", "FB", "FC", "LINE_FIX")):
@@ -1025,7 +1055,12 @@ def validate_x(seed=2):
 # 12 s + e, register r -> 144 + r), so the executor needs no address selects.
 SLOTS = ["F", "A", "B", "C", "D", "E", "G", "H", "I", "J", "K", "L"]   # enum S_F.. (bn256_pairing.h)
 F_BASE = 12 * len(SLOTS)
-SCR_BASE = {"FE": F_BASE + 2, "ML": 12 * SLOTS.index("C")}
+# register base per context: FOLD keeps only ZERO and ONE, right after slot B
+FOLD_F_BASE = 12 * (SLOTS.index("B") + 1)
+F_BASE_CTX = {"FE": F_BASE, "ML": F_BASE, "FOLD": FOLD_F_BASE}
+SCR_BASE = {"FE": F_BASE + 2, "ML": 12 * SLOTS.index("C"), "FOLD": FOLD_F_BASE + 2}
+REGION_END = {"FE": F_BASE + NREGS_RUNTIME, "ML": F_BASE + NREGS_RUNTIME,
+              "FOLD": FOLD_F_BASE + 2 + SCRATCH_CAP["FOLD"]}
 assert SCR_BASE["FE"] + SCRATCH_CAP["FE"] <= F_BASE + NREGS_RUNTIME
 
 
@@ -1054,7 +1089,9 @@ INSTANCES = sorted(set(
     + [(g, ()) for g in ("PDBL", "PADD_POS", "PADD_NEG", "PADD_F1", "PADD_F2", "PDBL_1")]
     + [(f"PADD_{v}_{i}", ()) for v in ("POS", "NEG", "F1", "F2") for i in (1, 3)]
     + [(f"MADD_{v}_2", ("F", "F")) for v in ("POS", "NEG", "F1", "F2")]
-    + [("MDBL_1", ("F", "F")), ("MDBL_2", ("F", "F"))]))
+    + [("MDBL_1", ("F", "F")), ("MDBL_2", ("F", "F"))]
+    # bn256_gt.hip: the sig-only Miller loop and the GT fold
+    + [("SDBL", ("F", "F")), ("LFEV", ("F", "F")), ("FEVAL", ()), ("MUL12F", ("A", "A", "B"))]))
 
 
 def bind(xr, binding, ctx):
@@ -1064,6 +1101,7 @@ def bind(xr, binding, ctx):
         D, A = binding
         B = A
     sbase = SCR_BASE[ctx]
+    fbase = F_BASE_CTX[ctx]
 
     def src(code):
         if code >= X_SCR:
@@ -1072,14 +1110,16 @@ def bind(xr, binding, ctx):
             return 12 * SLOTS.index(B) + (code - X_SLOT_B)
         if code >= SLOT_A:
             return 12 * SLOTS.index(A) + (code - SLOT_A)
-        return F_BASE + code
+        assert ctx != "FOLD" or code in (REG["ZERO"], REG["ONE"]), "FOLD keeps only ZERO and ONE"
+        return fbase + code
 
     def dst(code):
         if code == NONE:
             return NONE
         if code >= SLOT_A:
             return 12 * SLOTS.index(D) + (code - SLOT_A)
-        return F_BASE + code
+        assert ctx != "FOLD", "FOLD programs write slots only"
+        return fbase + code
 
     lanes = []
     for L in xr.lanes:
@@ -1095,7 +1135,7 @@ def bind(xr, binding, ctx):
         srcs = [u for u, v in L["prod"] + L.get("prod2", [])] + [v for u, v in L["prod"] + L.get("prod2", [])]
         srcs += [s_ for s_, _ in L["lin"] + L.get("lin2", [])] + [s_ for _, t in L["pre"] for s_, _ in t]
         for v in [L["dst"], L.get("dst2", NONE)] + [d for d, _ in L["pre"]] + srcs:
-            assert v == NONE or v < F_BASE + NREGS_RUNTIME, "index out of the kernels' team region"
+            assert v == NONE or v < REGION_END[ctx], "index out of the kernels' team region"
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
     out.ks1, out.ks2 = xr.ks1, xr.ks2
@@ -1124,11 +1164,12 @@ def check_instances(X, seed=3):
     rng = random.Random(seed)
     for name, binding in INSTANCES:
         ctx = X_PROGRAMS[name]
+        fb = F_BASE_CTX[ctx]
         rounds = [bind(xr, binding, ctx) for xr in X[name]]
         mem = [rng.randrange(P) for _ in range(F_BASE + NREGS)]
-        mem[F_BASE + REG["ZERO"]] = 0
-        mem[F_BASE + REG["ONE"]] = 1
-        F = {r: mem[F_BASE + r] for r in range(NREGS)}
+        mem[fb + REG["ZERO"]] = 0
+        mem[fb + REG["ONE"]] = 1
+        F = {r: mem[fb + r] for r in range(NREGS)}
         A = B = None
         if binding:
             bd = list(binding) + ([binding[1]] if len(binding) == 2 else [])
@@ -1141,7 +1182,7 @@ def check_instances(X, seed=3):
             assert all(mem[d0 + e] == v for e, v in want_D.items()), f"instance {name}{binding}"
         else:
             for r, v in F.items():
-                assert mem[F_BASE + r] == v, f"instance {name} reg {r}"
+                assert mem[fb + r] == v, f"instance {name} reg {r}"
 
 
 def emit_x(X, path):
@@ -1152,6 +1193,8 @@ def emit_x(X, path):
              "#define HG_P2N " + ", ".join("0x%08xu" % v for v in P2N),
              "enum XProg { " + ", ".join(f"XP_{n}" for n in X_PROGRAMS) + " };",
              f"static constexpr int kXFetchWords = {X_FETCH_WORDS};",
+             f"static constexpr int kFoldRegBase = {FOLD_F_BASE};  // FOLD team region: ZERO, ONE here",
+             f"static constexpr int kFoldTeamElems = {REGION_END['FOLD']};",
              "template <int PROG, int D = -1, int A = -1, int B = -1> struct XInst;"]
     words = []
     for name, binding in INSTANCES:
