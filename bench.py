@@ -58,6 +58,13 @@ G1_GEN_BYTES = (1).to_bytes(32, "big") + (P - 2).to_bytes(32, "big")
 FPMUL_PER_CHECK = 25271
 # one G2 mixed addition (madd-2007-bl: 7M2 + 4S2, Fp2 products as 3 Fp products)
 FPMUL_PER_G2_ADD = 29
+# The GT path (handel_amd/csrc/bn256_gt.hip) runs less than the reference
+# algorithm: per check ONE pairing (G2Base at -sig, table lines) and its final
+# exponentiation — the oracle's count with the pk side switched off
+# (tests/test_oracle.py pins it) — plus one Fp12 product per window-table term
+# of the fold (Karatsuba tower: 3 Fp6 x 6 Fp2 x 3 Fp products).
+FPMUL_PER_SIG_PAIRING = 19308
+FPMUL_PER_GT_MUL = 54
 # u32 x u32 multiply-adds per Fp multiplication (8-limb CIOS: 2*8^2 + 8)
 MADS_PER_FPMUL = 136
 # Peak v_mad_u64_u32 rate, measured by tools/intrate.hip on MI355X with 8
@@ -136,6 +143,35 @@ def make_aggregate_batch(eng: Engine, n_reg: int, n: int, seed: int, full: bool 
             np.array(signers), reg)
 
 
+def gt_fold_terms(reqs, words, n_reg: int) -> int:
+    """GT-table terms the fold multiplies for this batch (host restatement of
+    bn256_gt.hip k_gt_plan: nonzero 16-key windows of the bitset in
+    registry-aligned windows, or of its complement inside an aligned Handel
+    block when that has fewer, plus the block's own term)."""
+    levels = max(1, (n_reg - 1).bit_length())
+    total = 0
+    for off, bitlen, size, woff in reqs.tolist():
+        nw = (bitlen + 63) // 64
+        v = 0
+        for i, w in enumerate(words[woff:woff + nw].tolist()):
+            v |= int(w) << (64 * i)
+        v &= (1 << bitlen) - 1
+        if v == 0:
+            continue
+        sh = off & 15
+
+        def nz(x):
+            x <<= sh
+            return sum(1 for j in range(0, sh + bitlen, 16) if (x >> j) & 0xffff)
+
+        k = (bitlen - 1).bit_length() if bitlen > 1 else 0
+        aligned = k <= levels and off % (1 << k) == 0 and (bitlen == 1 << k or off + bitlen == n_reg)
+        m_set = nz(v)
+        m_unset = nz(((1 << bitlen) - 1) ^ v)
+        total += (m_unset + 1) if (aligned and k > 0 and m_unset < m_set) else m_set
+    return total
+
+
 def pmc_traffic(pattern: str):
     """HBM bytes per launch of the kernels matching `pattern`, summed, from the
     newest committed PMC summary (profiles/*_pmc.csv, tools/rocpd_summary.py):
@@ -182,6 +218,15 @@ def host_cpu():
     return threads, {"nproc": os.cpu_count(), "affinity": aff, "model": model}
 
 
+def _host_scale(per_core: float, info: dict) -> dict:
+    """The box gives one GPU's job a CPU share (the threads measured); the
+    whole host's rate is extrapolated per core (linear: the checks are
+    independent), and so is one GPU's share of the host (nproc / 8 GPUs)."""
+    nproc = info.get("nproc") or 1
+    return {"host_all_cores_extrapolated": round(per_core * nproc, 1),
+            "host_share_per_gpu_extrapolated": round(per_core * nproc / 8, 1)}
+
+
 def cpu_baseline_single(pks: bytes, sigs: bytes, expect: np.ndarray):
     """Config 2 on the reference algorithm restated in C (oracle/bn256_ref.c,
     'port'): two full pairings + GT compare per check."""
@@ -194,7 +239,7 @@ def cpu_baseline_single(pks: bytes, sigs: bytes, expect: np.ndarray):
     dt = time.perf_counter() - t0
     assert np.array_equal(codes, expect), "CPU oracle verdicts differ"
     return {"value": round(n / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
-            "per_core": round(n / dt / threads, 1), **info,
+            "per_core": round(n / dt / threads, 1), **info, **_host_scale(n / dt / threads, info),
             "sample": f"the same {n} checks (lib.Message, 1/8 tampered), reference algorithm "
                       f"(2 pairings + GT compare per check), {threads} threads, {dt:.2f} s wall"}
 
@@ -214,7 +259,7 @@ def cpu_baseline_aggregate(reg: bytes, reqs, words, sigs: bytes, expect: np.ndar
     dt = time.perf_counter() - t0
     assert np.array_equal(codes, expect[:m]), "CPU oracle verdicts differ"
     return {"value": round(m / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
-            "per_core": round(m / dt / threads, 1), **info,
+            "per_core": round(m / dt / threads, 1), **info, **_host_scale(m / dt / threads, info),
             "sample": f"the first {m} requests of the batch (same registry, bitsets, signatures), reference "
                       f"algorithm (one G2 addition per set bit + 2 pairings + GT compare), {threads} threads, "
                       f"{dt:.2f} s wall"}
@@ -259,6 +304,13 @@ class AggregateWorkload:
         self.eng, self.n, self.stream = eng, n, stream
         (self.reqs, self.words, self.sigs, self.expect, self.signers,
          self.reg) = make_aggregate_batch(eng, n_reg, n, seed, full=full)
+        # the per-(message, registry) GT tables, built outside the timed region
+        # (once per Handel run: the message and the registry are fixed)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        assert eng.prepare_aggregate() == 0
+        self.setup_ms = (time.perf_counter() - t0) * 1e3
+        self.terms = gt_fold_terms(self.reqs, self.words, n_reg)
         self.d_reqs = _dev_bytes(self.reqs.tobytes(), dev)
         self.d_words = _dev_bytes(self.words.tobytes(), dev)
         self.d_sigs = _dev_bytes(self.sigs, dev)
@@ -399,14 +451,20 @@ def main():
     # the dominant kernels of the step: the Combine fold (plan, order, fold,
     # finish) and the pairing check, on the reference's algorithmic work
     agg_ms = ph["fold"] + ph["verify"]
-    roof = roofline(head.fpmul, agg_ms, "k_agg_plan + k_agg_order + k_aggregate + k_agg_finish + k_verify",
-                    r"k_agg_|k_aggregate|k_verify",
-                    f"per check: {FPMUL_PER_G2_ADD} Fp-mul per set bit (G2 addition) + {FPMUL_PER_CHECK} "
-                    f"(pairing check), x {MADS_PER_FPMUL} u32 mads; mean {head.signers.mean():.1f} set bits")
+    roof = roofline(head.fpmul, agg_ms, "GT fold (k_gt_*) + k_verify_sig", r"k_gt_|k_verify",
+                    f"the REFERENCE algorithm's work per check (SURVEY.md 8(d)): {FPMUL_PER_G2_ADD} Fp-mul per set "
+                    f"bit (G2 addition) + {FPMUL_PER_CHECK} (two-pairing check), x {MADS_PER_FPMUL} u32 mads; mean "
+                    f"{head.signers.mean():.1f} set bits; the GT path runs less (roofline_k_verify, roofline_gt_fold)")
     roof["kernels_ms"] = {"fold": round(ph["fold"], 4), "k_verify": round(ph["verify"], 4),
                           "submit": round(ph["submit"], 4)}
-    roof_verify = roofline(n * FPMUL_PER_CHECK, ph["verify"], "k_verify", r"k_verify",
-                           f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads per check")
+    # the kernels' own work (what the GT path runs): the pairing check kernel
+    # and the GT fold, each on its implemented algorithmic Fp-mul count
+    roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph["verify"], "k_verify_sig", r"k_verify_sig",
+                           f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
+                           "+ final exponentiation, oracle op count)")
+    roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph["fold"], "k_gt_plan + k_gt_scan + k_gt_terms + "
+                         "k_gt_chunks + k_gt_combine", r"k_gt_",
+                         f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each)")
 
     extra = {}
     if not args.no_extra:
@@ -452,6 +510,7 @@ def main():
         del full
         # reload the headline registry (the full-registry workload replaced it)
         assert not eng.registry_load(head.reg).any()
+        assert eng.prepare_aggregate() == 0
         if args.pipeline > 1:
             # a verifier serving a continuous stream: batches in flight on several
             # HIP streams, one engine context (own workspaces) per stream
@@ -459,6 +518,7 @@ def main():
             for e in engs[1:]:
                 assert e.set_message(LIB_MESSAGE) == 0
                 assert not e.registry_load(head.reg).any()
+                assert e.prepare_aggregate() == 0
             streams = [stream] + [torch.cuda.Stream(dev) for _ in engs[1:]]
             codes_p = [head.d_codes] + [torch.zeros(n, dtype=torch.int32, device=dev) for _ in engs[1:]]
 
@@ -506,6 +566,11 @@ def main():
                        "parallelism": f"dp{world} (one batch per GPU, RCCL all_gather of verdict bitsets)"},
             "roofline": roof,
             "roofline_k_verify": roof_verify,
+            "roofline_gt_fold": roof_fold,
+            "setup": {"ms": round(head.setup_ms, 2), "what": "per (message, registry), outside the timed "
+                      f"region: e(H, pk_i) for {n_reg} keys + GT products of every 16-key window subset and aligned "
+                      "block (hg_prepare_aggregate)",
+                      "cold_value": round(n / ((head.setup_ms + dt / args.steps * 1e3) * 1e-3), 1)},
             "cpu_baseline": cpu,
             **extra,
         }

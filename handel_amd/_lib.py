@@ -53,6 +53,7 @@ SIGNATURES = {
     "hg_processing_error_string": (ctypes.c_char_p, [_I, _I]),
     "hg_registry_load": (_I, [_P, _P, _SZ, _P]),
     "hg_registry_size": (_SZ, [_P]),
+    "hg_prepare_aggregate": (_I, [_P]),
     "hg_set_message": (_I, [_P, _P, _SZ]),
     "hg_verify_batch": (_I, [_P, _P, _P, _SZ, _P]),
     "hg_verify_batch_msg": (_I, [_P, _P, _SZ, _P, _P, _SZ, _P]),

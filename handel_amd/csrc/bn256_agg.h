@@ -46,6 +46,26 @@ HG_DEV uint32_t nz_bytes(uint64_t x) {
   x |= x >> 1;
   return __popcll(x & 0x0101010101010101ull);
 }
+// The same for registry-aligned windows of W bits (W = 8: the byte windows
+// above; W = 16: the GT fold's 16-key windows, bn256_gt.hip)
+template <int W>
+HG_DEV uint64_t agg_rword_w(const AggRequest& q, const uint64_t* words, int v, bool comp) {
+  const int sh = (int)(q.offset & (uint32_t)(W - 1));
+  const uint64_t hi = agg_mask_word(q, words, v, comp);
+  if (sh == 0) return hi;
+  return (hi << sh) | (agg_mask_word(q, words, v - 1, comp) >> (64 - sh));
+}
+template <int W>
+HG_DEV uint32_t agg_nrwords_w(const AggRequest& q) {
+  return (q.bitlen + (q.offset & (uint32_t)(W - 1)) + 63) / 64;
+}
+HG_DEV uint32_t nz_halves(uint64_t x) {  // nonzero 16-bit quarters of x
+  x |= x >> 8;
+  x |= x >> 4;
+  x |= x >> 2;
+  x |= x >> 1;
+  return __popcll(x & 0x0001000100010001ull);
+}
 HG_DEV AggPlan agg_plan(const AggRequest& q, uint32_t cnt, uint32_t nz_set, uint32_t nz_unset, int nreg, int levels) {
   AggPlan p;
   p.cnt = cnt;

@@ -10,6 +10,9 @@ struct Gt {
   uint32_t w[120];
 };
 static constexpr int kGtChunk = 8;  // window-table values per fold chunk (one team)
+// The fold's windows: aligned 16-key windows, 65536 subset products each
+// (7.9 GB of HBM for a 4000-key registry; built from the 8-key tables)
+static constexpr int kGtWinBits = 16;
 
 // per-request fold plan (k_gt_plan, k_gt_scan)
 struct GtReq {
@@ -40,8 +43,9 @@ struct GtWork {
 
 // G_i = e(H, pk_i) for the n registry keys
 void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s);
-// win[256 w + s] = product of G_{8w + j} over the bits j of s (absent keys = 1)
-void launch_gt_windows(const Gt* key, int nreg, Gt* win, int nwin, hipStream_t s);
+// w8[256 w + s] = product of G_{8w + j} over the bits j of s (absent keys = 1);
+// then w16[65536 w + s] = product of G_{16w + j} over the bits j of s
+void launch_gt_windows(const Gt* key, int nreg, Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s);
 // dst[j] = src[2j] * src[2j + 1] (entries `stride` apart; a missing odd entry = 1)
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s);
 // the fold of n requests: y[r] = conj(e(H, aggregate key of r)); codes: level

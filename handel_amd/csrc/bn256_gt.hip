@@ -210,6 +210,35 @@ __global__ __launch_bounds__(64) void k_gt_cross(int nwin, Gt* win) {
   }
 }
 
+// 16-key windows: entry (hi << 8) | lo = w8[2w][lo] * w8[2w + 1][hi]; one
+// team per (window, hi), 256 products, the next left operand in flight.
+__global__ __launch_bounds__(64) void k_gt_win16(const Gt* w8, int nwin8, int nwin16, Gt* w16) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
+  Team T = make_team(lds, kFoldWords);
+  fold_regs_init(T);
+  const int task = blockIdx.x * 4 + ((threadIdx.x & 63) >> 4);
+  const bool valid = task < 256 * nwin16;
+  const int w = valid ? task >> 8 : 0, hi = task & 255;
+  const Gt* lo_tab = w8 + (size_t)(2 * w) * 256;
+  const bool has_hi = 2 * w + 1 < nwin8;
+  Gt* dst = w16 + (size_t)w * 65536 + (size_t)hi * 256;
+  XStream S = x_stream();
+  Fp hv, one, nxt;
+  gt_one_value(one, T);
+  gt_read(hv, w8 + (size_t)(has_hi ? 2 * w + 1 : 2 * w) * 256 + hi, T);
+  fp_sel(hv, has_hi, hv, one);
+  gt_read(nxt, lo_tab, T);
+#pragma unroll 1
+  for (int lo = 0; lo < 256; lo++) {
+    gt_put(T, S_A, nxt, false);
+    gt_put(T, S_B, hv, false);
+    if (lo + 1 < 256) gt_read(nxt, lo_tab + lo + 1, T);
+    fold_mul(T, S);
+    team_sync();
+    if (valid) gt_store(T, S_A, dst + lo);
+  }
+}
+
 // Block products, one level: dst[j] = src[2j] * src[2j + 1] (the last block of
 // a level may be clipped: src[2j + 1] absent -> 1). src entries `stride` apart.
 __global__ __launch_bounds__(64) void k_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst) {
@@ -228,24 +257,45 @@ __global__ __launch_bounds__(64) void k_gt_blocks(const Gt* src, int stride, int
 }
 
 // ------------------------------------------------------------------ the fold of a batch
-// Plan (one wave per request): set count, nonzero window bytes of the bitset
-// and of its complement, the complement decision (agg_plan, as the G2 fold),
-// the request's term count m and chunk count; an empty bitset is the
-// reference's nil-aggregate panic (HG_ERR_EMPTY_AGG).
-__global__ __launch_bounds__(64) void k_gt_plan(const AggRequest* reqs, int n, const uint64_t* words, int32_t* codes,
-                                                int nreg, int levels, GtReq* plan) {
-  const int r = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (r >= n) return;
+// Term encoding: bits 0..29 index a GT table, bit 30 = conjugate on load,
+// bit 31 = the block table (else the window table).
+static constexpr uint32_t kTermConj = 1u << 30, kTermBlk = 1u << 31, kTermIdx = kTermConj - 1;
+HG_DEV const Gt* term_ptr(uint32_t t, const Gt* win, const Gt* blk) {
+  return ((t & kTermBlk) ? blk : win) + (t & kTermIdx);
+}
+
+// Plan and terms (one wave per request). The pairing check compares with
+//   Y = conj(agg) = prod conj(t)                 (plain fold: conj is a ring
+//                                                  automorphism, so every term
+//                                                  is loaded conjugated)
+//   Y = conj(block * conj(prod)) = conj(block) * prod   (complemented fold:
+//                                                  conj(block) is one more term)
+// so a request is ONE product of m' = m + comp terms. Ranges in the batch's
+// term and chunk lists are taken with atomics (their order is irrelevant);
+// then the window-table index of every nonzero byte of the folded mask in
+// registry-aligned windows, and the owner of each chunk. An empty bitset is
+// the reference's nil-aggregate panic (HG_ERR_EMPTY_AGG).
+static constexpr int kPlanWaves = 16;  // requests per k_gt_plan workgroup (one wave each)
+__global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* reqs, int n, const uint64_t* words,
+                                                             int32_t* codes, int nreg, int levels, GtBlockIndex bi,
+                                                             GtReq* plan, GtHdr* hdr, uint32_t* terms,
+                                                             int* chunk_req) {
+  __shared__ int sm[kPlanWaves], sc[kPlanWaves], base_m, base_c;
+  const int wv = threadIdx.x >> 6;
+  const int r = blockIdx.x * kPlanWaves + wv;
+  const int lane = threadIdx.x & 63;
   GtReq g;
-  g.m = g.chunks = g.comp = g.k = 0;
-  if (codes[r] == HG_OK) {
-    const AggRequest q = reqs[r];
+  g.m = g.chunks = g.comp = g.k = g.term_off = g.chunk_off = 0;
+  AggRequest q;
+  q.offset = q.bitlen = q.level_size = q.word_offset = 0;
+  bool go = r < n && codes[r] == HG_OK;
+  if (go) {
+    q = reqs[r];
     uint32_t cnt = 0, nzs = 0, nzu = 0;
     for (uint32_t wi = lane; wi < (q.bitlen + 63) / 64; wi += 64) cnt += __popcll(agg_word(q, words, wi));
-    for (uint32_t v = lane; v < agg_nrwords(q); v += 64) {
-      nzs += nz_bytes(agg_rword(q, words, (int)v, false));
-      nzu += nz_bytes(agg_rword(q, words, (int)v, true));
+    for (uint32_t v = lane; v < agg_nrwords_w<kGtWinBits>(q); v += 64) {
+      nzs += nz_halves(agg_rword_w<kGtWinBits>(q, words, (int)v, false));
+      nzu += nz_halves(agg_rword_w<kGtWinBits>(q, words, (int)v, true));
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
@@ -256,72 +306,58 @@ __global__ __launch_bounds__(64) void k_gt_plan(const AggRequest* reqs, int n, c
     const AggPlan p = agg_plan(q, cnt, nzs, nzu, nreg, levels);
     if (cnt == 0) {
       if (lane == 0) codes[r] = HG_ERR_EMPTY_AGG;
+      go = false;
     } else {
-      g.m = (int)p.m;
-      g.chunks = (g.m + kGtChunk - 1) / kGtChunk;
       g.comp = p.comp ? 1 : 0;
       g.k = p.k;
+      g.m = (int)p.m + g.comp;
+      g.chunks = (g.m + kGtChunk - 1) / kGtChunk;
     }
   }
-  if (lane == 0) plan[r] = g;
-}
-
-// Exclusive prefix sums of the term and chunk counts (one block), totals in hdr.
-__global__ __launch_bounds__(1024) void k_gt_scan(int n, GtReq* plan, GtHdr* hdr) {
-  __shared__ int sm[1024], sc[1024];
-  __shared__ int carry_m, carry_c;
-  const int t = threadIdx.x;
-  if (t == 0) carry_m = carry_c = 0;
+  // ranges in the batch's term and chunk lists: one atomic per workgroup
+  if (lane == 0) {
+    sm[wv] = g.m;
+    sc[wv] = g.chunks;
+  }
   __syncthreads();
-  for (int base = 0; base < n; base += 1024) {
-    const int i = base + t;
-    const int m = i < n ? plan[i].m : 0, c = i < n ? plan[i].chunks : 0;
-    sm[t] = m;
-    sc[t] = c;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-      const int xm = t >= d ? sm[t - d] : 0, xc = t >= d ? sc[t - d] : 0;
-      __syncthreads();
-      sm[t] += xm;
-      sc[t] += xc;
-      __syncthreads();
+  if (threadIdx.x == 0) {
+    int tm = 0, tc = 0;
+    for (int i = 0; i < kPlanWaves; i++) {
+      const int m = sm[i], c = sc[i];
+      sm[i] = tm;
+      sc[i] = tc;
+      tm += m;
+      tc += c;
     }
-    if (i < n) {
-      plan[i].term_off = carry_m + sm[t] - m;
-      plan[i].chunk_off = carry_c + sc[t] - c;
-    }
-    __syncthreads();
-    if (t == 1023) {
-      carry_m += sm[t];
-      carry_c += sc[t];
-    }
-    __syncthreads();
+    base_m = tm ? atomicAdd(&hdr->terms, tm) : 0;
+    base_c = tc ? atomicAdd(&hdr->chunks, tc) : 0;
   }
-  if (t == 0) {
-    hdr->terms = carry_m;
-    hdr->chunks = carry_c;
-  }
-}
-
-// Terms (one wave per request): the window-table index 256 w + byte of every
-// nonzero byte of the folded mask in registry-aligned windows, in order; and
-// the owner of each of the request's chunks.
-__global__ __launch_bounds__(64) void k_gt_terms(const AggRequest* reqs, int n, const uint64_t* words,
-                                                 const int32_t* codes, const GtReq* plan, uint32_t* terms,
-                                                 int* chunk_req) {
-  const int r = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (r >= n || codes[r] != HG_OK) return;
-  const GtReq g = plan[r];
-  if (g.m == 0) return;
-  const AggRequest q = reqs[r];
-  const uint32_t nrw = agg_nrwords(q);
-  const uint32_t win0 = q.offset >> 3;
+  __syncthreads();
+  g.term_off = base_m + sm[wv];
+  g.chunk_off = base_c + sc[wv];
+  if (r < n && lane == 0) plan[r] = g;
+  if (!go) return;  // no barrier below
   uint32_t at = g.term_off;
+  if (g.comp) {
+    if (lane == 0) {
+      uint32_t t;
+      if (g.k <= 4) {  // a block inside one window: that window's subset entry
+        const uint32_t mask = ((1u << (1u << g.k)) - 1u) << (q.offset & 15u);
+        t = (q.offset >> 4) * 65536u + (mask & 0xffffu);
+      } else {
+        t = kTermBlk | (uint32_t)(bi.base[g.k] + (q.offset >> g.k));
+      }
+      terms[at] = t | kTermConj;
+    }
+    at++;
+  }
+  const uint32_t nrw = agg_nrwords_w<kGtWinBits>(q);
+  const uint32_t win0 = q.offset >> 4;
+  const uint32_t flag = g.comp ? 0u : kTermConj;
   for (uint32_t v0 = 0; v0 < nrw; v0 += 64) {
     const uint32_t v = v0 + lane;
-    const uint64_t mb = v < nrw ? agg_rword(q, words, (int)v, g.comp != 0) : 0;
-    const uint32_t pc = nz_bytes(mb);
+    const uint64_t mb = v < nrw ? agg_rword_w<kGtWinBits>(q, words, (int)v, g.comp != 0) : 0;
+    const uint32_t pc = nz_halves(mb);
     uint32_t inc = pc;  // inclusive prefix over the wave
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -330,22 +366,24 @@ __global__ __launch_bounds__(64) void k_gt_terms(const AggRequest* reqs, int n, 
     }
     uint32_t pos = at + inc - pc;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const uint32_t byte = (uint32_t)(mb >> (8 * j)) & 255u;
-      if (byte) terms[pos++] = (win0 + 8 * v + j) * 256u + byte;
+    for (int j = 0; j < 4; j++) {
+      const uint32_t half = (uint32_t)(mb >> (16 * j)) & 0xffffu;
+      if (half) terms[pos++] = ((win0 + 4 * v + j) * 65536u + half) | flag;
     }
     at += __shfl(inc, 63);
   }
   for (int c = lane; c < g.chunks; c += 64) chunk_req[g.chunk_off + c] = r;
 }
 
-// Chunks: each team multiplies the (at most kGtChunk) window-table values of
-// one chunk into a partial product. A fixed grid walks the chunk list (the
+// Chunks: each team multiplies the (at most kGtChunk) terms of one chunk. A
+// request of one chunk is finished here (its product is Y); the others leave
+// partial products for k_gt_combine. A fixed grid walks the chunk list (the
 // count is on the device); every wave runs to the same, wave-uniform bound.
 // The next term is fetched from HBM into registers while the current product
 // runs.
-__global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const uint32_t* terms, const int* chunk_req,
-                                                  const GtReq* plan, const GtHdr* hdr, Gt* partial) {
+__global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, const uint32_t* terms,
+                                                  const int* chunk_req, const GtReq* plan, const GtHdr* hdr,
+                                                  Gt* partial, Gt* y) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
   Team T = make_team(lds, kFoldWords);
   fold_regs_init(T);
@@ -355,48 +393,58 @@ __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const uint32_t*
   for (int base = blockIdx.x * 4; base < total; base += gridDim.x * 4) {  // wave-uniform
     const int c = base + team;
     const bool valid = c < total;
-    int first = 0, cnt = 0;
+    int first = 0, cnt = 0, r = 0;
+    bool single = false;
     if (valid) {
-      const GtReq g = plan[chunk_req[c]];
+      r = chunk_req[c];
+      const GtReq g = plan[r];
       first = g.term_off + (c - g.chunk_off) * kGtChunk;
       cnt = min(kGtChunk, g.term_off + g.m - first);
+      single = g.chunks == 1;
     }
     int maxc = cnt;
 #pragma unroll
     for (int d = 16; d < 64; d <<= 1) maxc = max(maxc, __shfl_xor(maxc, d));
-    gt_load_or_one(T, S_A, win + (valid ? terms[first] : 0), valid);
-    Fp nxt;
+    Fp cur, nxt, one;
+    gt_one_value(one, T);
     fp_zero(nxt);
-    if (1 < cnt) gt_read(nxt, win + terms[first + 1], T);
+    uint32_t t0 = valid ? terms[first] : 0u, t1 = 0u;
+    gt_read(cur, term_ptr(t0, win, blk), T);
+    fp_sel(cur, valid, cur, one);
+    gt_put(T, S_A, cur, (t0 & kTermConj) != 0);
+    if (1 < cnt) {
+      t1 = terms[first + 1];
+      gt_read(nxt, term_ptr(t1, win, blk), T);
+    }
 #pragma unroll 1
     for (int i = 1; i < maxc; i++) {
-      Fp one, v;
-      gt_one_value(one, T);
+      Fp v;
       fp_sel(v, i < cnt, nxt, one);
-      gt_put(T, S_B, v, false);
-      if (i + 1 < cnt) gt_read(nxt, win + terms[first + i + 1], T);  // in flight across the product
+      gt_put(T, S_B, v, i < cnt && (t1 & kTermConj) != 0);
+      if (i + 1 < cnt) {  // in flight across the product
+        t1 = terms[first + i + 1];
+        gt_read(nxt, term_ptr(t1, win, blk), T);
+      }
       fold_mul(T, S);
     }
     team_sync();
-    if (valid) gt_store(T, S_A, partial + c);
+    if (valid) gt_store(T, S_A, single ? y + r : partial + c);
     team_sync();
   }
 }
 
-// Combine (one wave per request): the 4 teams multiply every 4th partial, a
-// 2-level tree joins them, then the target of the pairing check:
-//   Y = conj(agg) = conj(prod)             (plain fold)
-//   Y = conj(block * conj(prod)) = conj(block) * prod   (complemented fold)
-__global__ __launch_bounds__(64) void k_gt_combine(const AggRequest* reqs, int n, const int32_t* codes,
-                                                   const GtReq* plan, const Gt* partial, const Gt* win,
-                                                   const Gt* blk, GtBlockIndex bi, Gt* y) {
+// Combine (one wave per request of two or more chunks): the 4 teams multiply
+// every 4th partial, a 2-level tree joins them into Y.
+__global__ __launch_bounds__(64) void k_gt_combine(int n, const int32_t* codes, const GtReq* plan,
+                                                   const Gt* partial, Gt* y) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
   const int r = blockIdx.x;
   if (r >= n || codes[r] != HG_OK) return;  // one request per wave: uniform
+  const GtReq g = plan[r];
+  if (g.chunks < 2) return;
   Team T = make_team(lds, kFoldWords);
   fold_regs_init(T);
   const int team = (threadIdx.x & 63) >> 4;
-  const GtReq g = plan[r];
   XStream S = x_stream();
   const int rounds = (g.chunks + 3) / 4;
   gt_load_or_one(T, S_A, partial + (team < g.chunks ? g.chunk_off + team : 0), team < g.chunks);
@@ -406,30 +454,10 @@ __global__ __launch_bounds__(64) void k_gt_combine(const AggRequest* reqs, int n
     gt_load_or_one(T, S_B, partial + (c < g.chunks ? g.chunk_off + c : 0), c < g.chunks);
     fold_mul(T, S);
   }
-  if (g.chunks > 1) {
-    for (int d = 1; d < 4; d <<= 1) {
-      team_sync();
-      lds_fp12_copy(T, slot(T, S_B), lds + (team ^ d) * kFoldWords + S_A * kFp12Words);
-      fold_mul(T, S);
-    }
-  }
-  team_sync();
-  if (g.comp) {
-    const AggRequest q = reqs[r];
-    const Gt* B;
-    if (g.k <= 3) {  // a block inside one window: that window's subset entry
-      const uint32_t mask = ((1u << (1u << g.k)) - 1u) << (q.offset & 7u);
-      B = win + (size_t)(q.offset >> 3) * 256 + (mask & 255u);
-    } else {
-      B = blk + bi.base[g.k] + (q.offset >> g.k);
-    }
-    gt_load(T, S_B, B, true);
-    fold_mul(T, S);
-  } else {
-    Fp v;
-    ld_fp_a8(v, slot(T, S_A) + T.e * 10);
+  for (int d = 1; d < (g.chunks > 2 ? 4 : 2); d <<= 1) {
     team_sync();
-    gt_put(T, S_A, v, true);
+    lds_fp12_copy(T, slot(T, S_B), lds + (team ^ d) * kFoldWords + S_A * kFp12Words);
+    fold_mul(T, S);
   }
   team_sync();
   if (team == 0) gt_store(T, S_A, y + r);
@@ -545,10 +573,11 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, int n, c
 void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s) {
   if (n > 0) k_gt_keys<4><<<nblk(n, 4), 64, 0, s>>>(reg, n, tab, h, out);
 }
-void launch_gt_windows(const Gt* key, int nreg, Gt* win, int nwin, hipStream_t s) {
-  if (nwin <= 0) return;
-  k_gt_nib<<<nblk(2 * nwin, 4), 64, 0, s>>>(key, nreg, nwin, win);
-  k_gt_cross<<<nblk(15 * nwin, 4), 64, 0, s>>>(nwin, win);
+void launch_gt_windows(const Gt* key, int nreg, Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s) {
+  if (nwin8 <= 0) return;
+  k_gt_nib<<<nblk(2 * nwin8, 4), 64, 0, s>>>(key, nreg, nwin8, w8);
+  k_gt_cross<<<nblk(15 * nwin8, 4), 64, 0, s>>>(nwin8, w8);
+  k_gt_win16<<<nblk(256 * nwin16, 4), 64, 0, s>>>(w8, nwin8, nwin16, w16);
 }
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s) {
   if (ndst > 0) k_gt_blocks<<<nblk(ndst, 4), 64, 0, s>>>(src, stride, nsrc, dst, ndst);
@@ -556,11 +585,11 @@ void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hi
 void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_t* codes, int nreg, int levels,
                     const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, hipStream_t s) {
   if (n <= 0) return;
-  k_gt_plan<<<n, 64, 0, s>>>(reqs, n, words, codes, nreg, levels, w.plan);
-  k_gt_scan<<<1, 1024, 0, s>>>(n, w.plan, w.hdr);
-  k_gt_terms<<<n, 64, 0, s>>>(reqs, n, words, codes, w.plan, w.terms, w.chunk_req);
-  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, w.terms, w.chunk_req, w.plan, w.hdr, w.partial);
-  k_gt_combine<<<n, 64, 0, s>>>(reqs, n, codes, w.plan, w.partial, win, blk, bi, y);
+  (void)hipMemsetAsync(w.hdr, 0, sizeof(GtHdr), s);
+  k_gt_plan<<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan, w.hdr,
+                                                            w.terms, w.chunk_req);
+  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.chunk_req, w.plan, w.hdr, w.partial, y);
+  k_gt_combine<<<n, 64, 0, s>>>(n, codes, w.plan, w.partial, y);
 }
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
   if (n > 0) k_verify_sig<4><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, y, codes);

@@ -178,7 +178,7 @@ struct hg_ctx {
   // subset products and block products, valid for the current message and
   // registry (rebuilt by the first aggregate submission after either changes)
   bool gt_ready = false;
-  DevBuf<Gt> gt_key, gt_win, gt_blk;
+  DevBuf<Gt> gt_key, gt_w8, gt_win, gt_blk;  // gt_w8: 8-key windows, gt_win: 16-key windows
   GtBlockIndex gt_bi{};
   // GT fold workspaces
   DevBuf<GtReq> gt_plan;
@@ -284,6 +284,7 @@ static void release_all(hg_ctx* c) {
   c->agg_ws.release();
   c->words.release();
   c->gt_key.release();
+  c->gt_w8.release();
   c->gt_win.release();
   c->gt_blk.release();
   c->gt_plan.release();
@@ -384,6 +385,10 @@ static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector
   }
 }
 
+// The GT tables take ~1.97 MB of HBM per registry key (16-key windows of
+// 65536 GT values): registries up to 16384 keys (32 GB) use the GT path,
+// larger ones the G2 point fold.
+static constexpr size_t kGtMaxRegistry = 16384;
 // Which fold verifies aggregate requests: the GT path (bn256_gt.hip, default)
 // or the G2 point fold + k_verify (HG_AGG_PATH=g2, kept for A/B runs).
 static bool gt_path_enabled() {
@@ -399,21 +404,23 @@ static bool gt_path_enabled() {
 // registry, on stream s (inside a submission).
 static int build_gt_locked(hg_ctx* c, hipStream_t s) {
   const int n = (int)c->nreg;
-  const int nwin = (n + 7) / 8;
+  const int nwin8 = (n + 7) / 8, nwin16 = (n + 15) / 16;
   HG_CHECK(c, c->gt_key.ensure(n));
-  HG_CHECK(c, c->gt_win.ensure((size_t)nwin * 256));
+  HG_CHECK(c, c->gt_w8.ensure((size_t)nwin8 * 256));
+  HG_CHECK(c, c->gt_win.ensure((size_t)nwin16 * 65536));
+  // blocks of level k >= 5 (levels <= 4 are 16-key window entries)
   int cnt[24] = {0};
   int total = 0;
-  for (int k = 4; k <= c->block_levels && k < 24; k++) {
+  for (int k = 5; k <= c->block_levels && k < 24; k++) {
     cnt[k] = (int)(((size_t)n + ((size_t)1 << k) - 1) >> k);
     c->gt_bi.base[k] = total;
     total += cnt[k];
   }
   if (total) HG_CHECK(c, c->gt_blk.ensure(total));
   launch_gt_keys(c->reg.p, n, c->d_lines, c->d_h, c->gt_key.p, s);
-  launch_gt_windows(c->gt_key.p, n, c->gt_win.p, nwin, s);
-  for (int k = 4; k <= c->block_levels && k < 24; k++) {
-    if (k == 4) launch_gt_blocks(c->gt_win.p + 255, 256, nwin, c->gt_blk.p + c->gt_bi.base[4], cnt[4], s);
+  launch_gt_windows(c->gt_key.p, n, c->gt_w8.p, nwin8, c->gt_win.p, nwin16, s);
+  for (int k = 5; k <= c->block_levels && k < 24; k++) {
+    if (k == 5) launch_gt_blocks(c->gt_win.p + 0xffff, 65536, nwin16, c->gt_blk.p + c->gt_bi.base[5], cnt[5], s);
     else launch_gt_blocks(c->gt_blk.p + c->gt_bi.base[k - 1], 1, cnt[k - 1], c->gt_blk.p + c->gt_bi.base[k], cnt[k], s);
   }
   int rc = check_launch(c);
@@ -423,9 +430,9 @@ static int build_gt_locked(hg_ctx* c, hipStream_t s) {
 }
 
 // GT fold workspaces for n requests: a request's folded mask has at most
-// 8 * (registry-aligned words) nonzero window bytes
+// 4 nonzero 16-bit windows per registry-aligned 64-bit word, plus the block term
 static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
-  const size_t mmax = 8 * ((c->nreg + 7 + 63) / 64 + 1);
+  const size_t mmax = 4 * ((c->nreg + 15 + 63) / 64 + 1) + 1;  // nonzero 16-bit windows + the block term
   const size_t cmax = (mmax + kGtChunk - 1) / kGtChunk;
   HG_CHECK(c, c->gt_plan.ensure(n));
   HG_CHECK(c, c->gt_hdr.ensure(1));
@@ -453,7 +460,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   }
   // GT path: the verdict needs no aggregate key in G2; the G2 fold still runs
   // when the caller wants the aggregate keys' marshals
-  const bool use_gt = verify && gt_path_enabled() && !c->hash_eof && c->nreg > 0;
+  const bool use_gt = verify && gt_path_enabled() && !c->hash_eof && c->nreg > 0 && c->nreg <= kGtMaxRegistry;
   const bool g2_fold = !use_gt || d_agg;
   GtWork gw{};
   if (use_gt) {
@@ -726,6 +733,25 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   c->block_levels = K;
   c->nreg = n;
+  return HG_OK;
+}
+
+int hg_prepare_aggregate(hg_ctx* c) {
+  if (!c) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->has_msg || c->nreg == 0) {
+    c->err = "hg_prepare_aggregate: needs a message and a registry";
+    return HG_ERR_ARG;
+  }
+  if (c->nreg > kGtMaxRegistry || !gt_path_enabled()) return HG_OK;  // aggregates use the G2 fold
+  if (c->hash_eof) return HG_ERR_HASH_EOF;
+  if (c->gt_ready) return HG_OK;
+  HG_CHECK(c, hipSetDevice(c->device));
+  HG_CHECK(c, begin(c, c->stream));
+  int rc = build_gt_locked(c, c->stream);
+  if (rc) return rc;
+  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
 

@@ -83,6 +83,12 @@ class Engine:
         return self._check(self.L.hg_set_message(self.ctx, _ptr(m) if len(m) else None, len(m)),
                            "hg_set_message", ok=(0, _lib.HG_ERR_HASH_EOF))
 
+    def prepare_aggregate(self) -> int:
+        """Builds the GT tables of aggregate verification for the current
+        message and registry now (hg_prepare_aggregate); HG_OK or HG_ERR_HASH_EOF."""
+        return self._check(self.L.hg_prepare_aggregate(self.ctx), "hg_prepare_aggregate",
+                           ok=(0, _lib.HG_ERR_HASH_EOF))
+
     def registry_load(self, pks: bytes) -> np.ndarray:
         a = _u8(pks)
         n = len(a) // 128
@@ -135,6 +141,21 @@ class Engine:
                                                len(words), _ptr(s), _ptr(codes), _ptr(agg)),
                     "hg_verify_aggregate")
         return (codes, agg.tobytes()) if want_agg else codes
+
+    def verify_aggregate_msg(self, msg: bytes, reqs: np.ndarray, words: np.ndarray, sigs: bytes):
+        """verify_aggregate with the message given per call: hashing and the
+        batch under one lock hold of the context (hg_verify_aggregate_msg)."""
+        reqs = np.ascontiguousarray(reqs, dtype=REQ_DTYPE)
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        m, s = _u8(msg), _u8(sigs)
+        n = len(reqs)
+        codes = np.zeros(n, dtype=np.int32)
+        self._check(self.L.hg_verify_aggregate_msg(self.ctx, _ptr(m) if len(m) else None, len(m),
+                                                   _ptr(reqs) if n else None, n,
+                                                   _ptr(words) if len(words) else None, len(words),
+                                                   _ptr(s) if n else None, _ptr(codes) if n else None, None),
+                    "hg_verify_aggregate_msg")
+        return codes
 
     def verify_multisig(self, bitlens, word_offsets, words: np.ndarray, sigs: bytes) -> np.ndarray:
         """VerifyMultiSignature (crypto.go:120-137) x n (hg_verify_multisig)."""

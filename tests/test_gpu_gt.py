@@ -1,0 +1,184 @@
+"""GPU suite: the GT path of aggregate verification (handel_amd/csrc/bn256_gt.hip).
+
+hg_verify_aggregate checks e(H, sum of set keys) == e(sig, G2Base) as
+FE(Miller(G2Base at -sig)) == conj(prod of per-key GT values), with the
+per-key values e(H, pk_i) and their window/block products built once per
+(message, registry). These tests pin the table life cycle (message and
+registry changes, hg_prepare_aggregate) and the GT verdicts against the C
+restatement of the reference (oracle/bn256_ref.c) and against the G2 point
+fold (HG_AGG_PATH=g2, run in a child process).
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from handel_amd._lib import HG_ERR_HASH_EOF, HandelGPUError
+from handel_amd.engine import REQ_DTYPE
+from oracle import bn256_oracle as O
+from oracle import ref_lib as R
+from tests import _fixtures as F
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _batch(ks, reg_n, msg, ranges, rng, tamper_every=5):
+    """Aggregate signatures of random bitsets over the given ranges, signed on msg."""
+    bitsets = F.random_bitsets(rng, [s for _, s in ranges])
+    for b in bitsets:
+        b[int(rng.integers(len(b)))] = True
+    h = O.hashed_message(msg)[0]
+    sigs = bytearray()
+    for (off, _), bits in zip(ranges, bitsets):
+        k = sum(ks[off + i] for i, b in enumerate(bits) if b) % O.ORDER
+        sigs += O.g1_marshal(O.g1_mul(h, k))
+    sigs = F.tamper(bytes(sigs), every=tamper_every)
+    reqs, words = F.pack_requests(ranges, bitsets)
+    return np.array(reqs, dtype=REQ_DTYPE), words, sigs
+
+
+def _levels(n_reg, nodes):
+    out = []
+    for node in nodes:
+        for lvl in range(1, O.log2_ceil(n_reg) + 1):
+            rl, err = O.range_level(node, n_reg, lvl)
+            if err is None:
+                out.append((rl[0], rl[1] - rl[0]))
+    return sorted(set(out)) + [(0, n_reg)]
+
+
+def _oracle(msg, reg, reqs, words, sigs):
+    return R.verify_aggregate(msg, reg, reqs["offset"], reqs["bitlen"], reqs["level_size"], words,
+                              reqs["word_offset"].astype(np.uint64), sigs, nthreads=8)
+
+
+def test_prepare_aggregate_states(engine):
+    """hg_prepare_aggregate: needs a message and a registry; a hash-rejected
+    message has nothing to build; otherwise builds (and then reuses) the tables."""
+    ks = F.scalars(20, seed=b"gt-prep")
+    reg = R.g2_scalar_base(F.scalar_bytes(ks))
+    assert list(engine.registry_load(reg)) == [0] * 20
+    assert engine.set_message(F.REJECT_MESSAGES[0]) == HG_ERR_HASH_EOF
+    assert engine.prepare_aggregate() == HG_ERR_HASH_EOF
+    assert engine.set_message(F.LIB_MESSAGE) == 0
+    assert engine.prepare_aggregate() == 0
+    assert engine.prepare_aggregate() == 0  # cached
+
+
+def test_prepare_aggregate_without_registry(engine_cf):
+    """A context whose registry failed to load has no registry: HG_ERR_ARG."""
+    bad = bytes([0xff]) * 128
+    engine_cf.registry_load(bad)
+    assert engine_cf.set_message(F.LIB_MESSAGE) == 0
+    with pytest.raises(HandelGPUError, match="hg_prepare_aggregate"):
+        engine_cf.prepare_aggregate()
+
+
+def test_tables_follow_message_and_registry(engine):
+    """The tables are e(H, .) of the CURRENT message and registry: switching
+    either rebuilds them, so signatures verify exactly under their own
+    message / registry (and a message's signatures fail under another)."""
+    rng = np.random.default_rng(3)
+    msgs = [F.LIB_MESSAGE, F.TEST_MESSAGES[0]]
+    regs = []
+    for seed in (b"gt-regA", b"gt-regB"):
+        ks = F.scalars(96, seed=seed)
+        regs.append((ks, R.g2_scalar_base(F.scalar_bytes(ks))))
+    ranges = _levels(96, (0, 41, 95))
+    for ri, (ks, reg) in enumerate(regs):
+        assert list(engine.registry_load(reg)) == [0] * 96
+        for mi, msg in enumerate(msgs):
+            reqs, words, sigs = _batch(ks, 96, msg, ranges, rng)
+            for use in msgs:  # the same signatures under both messages
+                codes = engine.verify_aggregate_msg(use, reqs, words, sigs)
+                want = _oracle(use, reg, reqs, words, sigs)
+                assert list(codes) == list(want), (ri, mi, use)
+                if use == msg:
+                    assert (np.asarray(codes) == 0).sum() > len(ranges) // 2
+                else:
+                    assert (np.asarray(codes) == 0).sum() == 0
+
+
+def test_gt_and_g2_paths_agree():
+    """The GT path (this process) and the G2 point fold + two-pairing check
+    (HG_AGG_PATH=g2, a child process) give the oracle's verdicts on the same
+    batch: 1024 multisigs at random Handel levels of a 1000-key registry."""
+    code = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, %r)
+import bench
+from handel_amd.engine import Engine
+e = Engine(device=0, flavor="go")
+assert e.set_message(bench.LIB_MESSAGE) == 0
+reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(e, 1000, 1024, seed=5)
+print(json.dumps([int(c) for c in e.verify_aggregate(reqs, words, sigs)]))
+""" % ROOT
+    outs = {}
+    for path in ("gt", "g2"):
+        env = dict(os.environ, HG_AGG_PATH=path)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[path] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert outs["gt"] == outs["g2"]
+    import bench
+    from handel_amd.engine import Engine
+
+    e = Engine(device=0, flavor="go")
+    try:
+        assert e.set_message(bench.LIB_MESSAGE) == 0
+        reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(e, 1000, 1024, seed=5)
+    finally:
+        e.close()
+    assert outs["gt"] == [int(c) for c in expect]
+    assert outs["gt"] == [int(c) for c in _oracle(bench.LIB_MESSAGE, reg, reqs, words, sigs)]
+
+
+def test_sig_edge_cases_on_gt_path(engine):
+    """Signature-side edge cases through the GT check: infinity signature
+    (valid only for an aggregate key at infinity), off-curve signature
+    (decode error), and a duplicated key folded twice."""
+    n = 64
+    ks = F.scalars(n, seed=b"gt-edge")
+    ks[9] = ks[8]
+    reg = bytearray(R.g2_scalar_base(F.scalar_bytes(ks)))
+    reg[128 * 20:128 * 21] = bytes(128)  # a registry key at infinity
+    reg = bytes(reg)
+    assert list(engine.registry_load(reg)) == [0] * n
+    msg = F.LIB_MESSAGE
+    assert engine.set_message(msg) == 0
+    h = O.hashed_message(msg)[0]
+    cases = [  # (offset, size, set bits, signature)
+        (8, 8, [0, 1], None),          # keys 8 and 9 are equal: 2 k8 H
+        (16, 8, [4], "inf"),           # only the infinity key: aggregate = infinity
+        (16, 8, [4], None),            # ... with the honest signature (also infinity)
+        (16, 8, [3, 4], None),         # infinity key beside a real one
+        (0, 64, list(range(64)), None),
+        (32, 32, list(range(32)), "offcurve"),
+        (0, 8, [1], "inf"),            # infinity signature on a real key: invalid
+    ]
+    ranges, bitsets, sigs = [], [], bytearray()
+    for off, size, bits, kind in cases:
+        ranges.append((off, size))
+        b = [False] * size
+        for i in bits:
+            b[i] = True
+        bitsets.append(b)
+        k = sum(0 if off + i == 20 else ks[off + i] for i in bits) % O.ORDER
+        if kind == "inf":
+            sigs += bytes(64)
+        elif kind == "offcurve":
+            sigs += (1).to_bytes(32, "big") + (1).to_bytes(32, "big")
+        else:
+            sigs += O.g1_marshal(O.g1_mul(h, k)) if k else bytes(64)
+    reqs, words = F.pack_requests(ranges, bitsets)
+    reqs = np.array(reqs, dtype=REQ_DTYPE)
+    codes = engine.verify_aggregate(reqs, words, bytes(sigs))
+    want = _oracle(msg, reg, reqs, words, bytes(sigs))
+    assert list(codes) == list(want)
+    assert list(codes[:5]) == [0, 0, 0, 0, 0] and codes[6] == 1

@@ -174,6 +174,25 @@ def test_algorithmic_work_per_check_is_pinned():
     assert (counts[1] - counts[0]) // 2 == bench.FPMUL_PER_CHECK
 
 
+def test_sig_pairing_work_is_pinned():
+    """The GT path's check kernel (k_verify_sig) runs one pairing, G2Base at
+    -sig, and its final exponentiation: the oracle's count of the same check
+    with the pk side off (pk = infinity) is bench.FPMUL_PER_SIG_PAIRING."""
+    import bench
+
+    L = R.lib()
+    L.ref_fp_mul_count.restype = ctypes.c_uint64
+    _, _, sigs = F.keys_and_sigs(3, seed=b"cnt")
+    inf = bytes(128 * 3)
+    counts = []
+    for n in (1, 3):
+        L.ref_reset_count(1)
+        R.verify_batch(F.LIB_MESSAGE, inf[:128 * n], sigs[:64 * n], nthreads=1, fast=2)
+        counts.append(L.ref_fp_mul_count())
+    L.ref_reset_count(0)
+    assert (counts[1] - counts[0]) // 2 == bench.FPMUL_PER_SIG_PAIRING
+
+
 # ------------------------------------------------------------------ Handel-level helpers
 def test_range_level_matches_partitioner_table():
     """The reference's own table: partitioner_test.go:296-343 TestPartitionerBinTreeRangeAt (n = 17)."""

@@ -10,7 +10,7 @@ mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 B="bench.py --steps 5 --warmup 2 --no-cpu --no-extra"
-K="k_verify|k_aggregate|k_agg_"
+K="k_verify|k_aggregate|k_agg_|k_gt_"
 timeout -k 10 300 python3 $B > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run -- python3 $B > $OUT/ktrace.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $OUT/fetch -o run -- python3 $B > $OUT/fetch.log 2>&1 &&
