@@ -451,7 +451,8 @@ def main():
     # the dominant kernels of the step: the Combine fold (plan, order, fold,
     # finish) and the pairing check, on the reference's algorithmic work
     agg_ms = ph["fold"] + ph["verify"]
-    roof = roofline(head.fpmul, agg_ms, "GT fold (k_gt_*) + k_verify_sig", r"k_gt_|k_verify",
+    roof = roofline(head.fpmul, agg_ms, "GT fold (k_gt_plan, k_gt_chunks, k_gt_combine) + k_verify_sig",
+                    r"k_gt_(plan|chunks|combine)|k_verify_sig",
                     f"the REFERENCE algorithm's work per check (SURVEY.md 8(d)): {FPMUL_PER_G2_ADD} Fp-mul per set "
                     f"bit (G2 addition) + {FPMUL_PER_CHECK} (two-pairing check), x {MADS_PER_FPMUL} u32 mads; mean "
                     f"{head.signers.mean():.1f} set bits; the GT path runs less (roofline_k_verify, roofline_gt_fold)")
@@ -462,8 +463,8 @@ def main():
     roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph["verify"], "k_verify_sig", r"k_verify_sig",
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
                            "+ final exponentiation, oracle op count)")
-    roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph["fold"], "k_gt_plan + k_gt_scan + k_gt_terms + "
-                         "k_gt_chunks + k_gt_combine", r"k_gt_",
+    roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
+                         r"k_gt_(plan|chunks|combine)",
                          f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each)")
 
     extra = {}
