@@ -493,6 +493,32 @@ def main():
             except Exception as e:  # pragma: no cover - reported, not fatal
                 extra["single"]["cpu_baseline"] = {"error": str(e)}
         del single
+        # config 2 with registry keys (the p2p aggregator's verifyPacket,
+        # simul/p2p/aggregator.go:244): one-key aggregate requests on the head
+        # registry, so each check is the GT path's single pairing
+        rng = np.random.default_rng(4242 + rank)
+        idx = rng.integers(0, n_reg, size=n)
+        kb = np.frombuffer(seeded_scalars(n_reg, 4321 + rank), dtype=np.uint8).reshape(n_reg, 32)
+        rsigs = bytearray(eng.sign(kb[idx].tobytes()))
+        rexpect = _tamper(eng, rsigs, n)
+        rreqs = np.array([(int(i), 1, 1, j) for j, i in enumerate(idx)], dtype=REQ_DTYPE)
+        rwords = np.ones(n, dtype=np.uint64)
+        d_rreqs, d_rwords = _dev_bytes(rreqs.tobytes(), dev), _dev_bytes(rwords.tobytes(), dev)
+        d_rsigs = _dev_bytes(bytes(rsigs), dev)
+        rcodes = torch.zeros(n, dtype=torch.int32, device=dev)
+
+        def rstep():
+            eng.verify_aggregate_device(d_rreqs.data_ptr(), n, d_rwords.data_ptr(), d_rsigs.data_ptr(),
+                                        rcodes.data_ptr(), 0, stream.cuda_stream)
+
+        rdt = timer.run(rstep, args.steps, args.warmup)
+        assert np.array_equal(rcodes.cpu().numpy(), rexpect), "registry single-signature verdicts"
+        extra["single_registry"] = {
+            "metric": "BN254 single-sig verifications/sec, registry keys (batch 4096)",
+            "value": round(n * args.steps * world / rdt, 1), "unit": "verifications/s",
+            "ms_per_step": round(rdt / args.steps * 1e3, 4),
+            "workload": f"{n} single signatures from random nodes of the {n_reg}-key registry (one-key aggregate "
+                        "requests: the GT path), lib.Message, 1/8 tampered"}
         # VerifyMultiSignature shape: every request spans the whole registry
         full = AggregateWorkload(eng, n_reg, n, seed=8765 + rank, dev=dev, stream=stream, full=True)
         fdt = timer.run(full.submit, args.steps, args.warmup)

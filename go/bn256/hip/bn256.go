@@ -279,6 +279,11 @@ func (p *PublicKey) VerifySignature(msg []byte, sig handel.Signature) error {
 		n := p.reg.size
 		return p.e.submit(msg, &Request{Offset: 0, LevelSize: n, BitLen: n, Words: p.bits, Sig: s}, nil)
 	}
+	if p.reg != nil && p.idx >= 0 {
+		// a registry key (the p2p aggregator's verifyPacket, simul/p2p/aggregator.go:244):
+		// a one-key aggregate request, so the check uses the precomputed e(H, pk)
+		return p.e.submit(msg, &Request{Offset: p.idx, LevelSize: 1, BitLen: 1, Words: []uint64{1}, Sig: s}, nil)
+	}
 	return p.e.submit(msg, nil, &single{pk: p.p, sig: s})
 }
 
