@@ -171,6 +171,24 @@ func (e *Engine) SetMessage(msg []byte) error {
 	return e.fail(rc)
 }
 
+// PrepareAggregate makes msg the context's message and builds the tables of
+// aggregate verification for it and the loaded registry now (e(H, pk_i) and
+// the GT window/block products: ≈ 15 ms for 4000 keys) instead of in the
+// first aggregate call. Call it once per Handel run after LoadRegistry.
+func (e *Engine) PrepareAggregate(msg []byte) error {
+	if err := e.SetMessage(msg); err != nil {
+		return err
+	}
+	switch rc := C.hg_prepare_aggregate(e.ctx); rc {
+	case C.HG_OK:
+		return nil
+	case C.HG_ERR_HASH_EOF:
+		return e.CodeError(codeHashEOF)
+	default:
+		return e.fail(rc)
+	}
+}
+
 // VerifyBatch runs n = len(sigs)/64 independent PublicKey.VerifySignature(msg,
 // sig) checks (bn256/go/bn256.go:82-94) in one launch; pks holds n 128-byte
 // key marshals. Hashing and checking happen under one lock hold of the
