@@ -9,7 +9,7 @@ namespace hg {
 struct Gt {
   uint32_t w[120];
 };
-static constexpr int kGtChunk = 8;  // window-table values per fold chunk (one team)
+static constexpr int kGtChunk = 8;  // default window-table values per fold chunk (one team)
 // The fold's windows: aligned 16-key windows, 65536 subset products each
 // (7.9 GB of HBM for a 4000-key registry; built from the 8-key tables)
 static constexpr int kGtWinBits = 16;
@@ -17,7 +17,7 @@ static constexpr int kGtWinBits = 16;
 // per-request fold plan (k_gt_plan, k_gt_scan)
 struct GtReq {
   int m;          // window-table terms of the folded mask
-  int chunks;     // ceil(m / kGtChunk)
+  int chunks;     // ceil(m / chunk)
   int comp;       // folded over the complement inside the aligned block of level k
   int k;
   int term_off;   // first term in the batch's term list
@@ -39,6 +39,7 @@ struct GtWork {
   int* chunk_req;
   Gt* partial;
   int chunk_grid;  // workgroups of k_gt_chunks (4 teams each)
+  int chunk;       // terms per chunk
 };
 
 // G_i = e(H, pk_i) for the n registry keys

@@ -279,7 +279,7 @@ static constexpr int kPlanWaves = 16;  // requests per k_gt_plan workgroup (one 
 __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* reqs, int n, const uint64_t* words,
                                                              int32_t* codes, int nreg, int levels, GtBlockIndex bi,
                                                              GtReq* plan, GtHdr* hdr, uint32_t* terms,
-                                                             int* chunk_req) {
+                                                             int* chunk_req, int chunk) {
   __shared__ int sm[kPlanWaves], sc[kPlanWaves], base_m, base_c;
   const int wv = threadIdx.x >> 6;
   const int r = blockIdx.x * kPlanWaves + wv;
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
       g.comp = p.comp ? 1 : 0;
       g.k = p.k;
       g.m = (int)p.m + g.comp;
-      g.chunks = (g.m + kGtChunk - 1) / kGtChunk;
+      g.chunks = (g.m + chunk - 1) / chunk;
     }
   }
   // ranges in the batch's term and chunk lists: one atomic per workgroup
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
   for (int c = lane; c < g.chunks; c += 64) chunk_req[g.chunk_off + c] = r;
 }
 
-// Chunks: each team multiplies the (at most kGtChunk) terms of one chunk. A
+// Chunks: each team multiplies the (at most `chunk`) terms of one chunk. A
 // request of one chunk is finished here (its product is Y); the others leave
 // partial products for k_gt_combine. A fixed grid walks the chunk list (the
 // count is on the device); every wave runs to the same, wave-uniform bound.
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
 // runs.
 __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, const uint32_t* terms,
                                                   const int* chunk_req, const GtReq* plan, const GtHdr* hdr,
-                                                  Gt* partial, Gt* y) {
+                                                  int chunk, Gt* partial, Gt* y) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
   Team T = make_team(lds, kFoldWords);
   fold_regs_init(T);
@@ -398,8 +398,8 @@ __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, 
     if (valid) {
       r = chunk_req[c];
       const GtReq g = plan[r];
-      first = g.term_off + (c - g.chunk_off) * kGtChunk;
-      cnt = min(kGtChunk, g.term_off + g.m - first);
+      first = g.term_off + (c - g.chunk_off) * chunk;
+      cnt = min(chunk, g.term_off + g.m - first);
       single = g.chunks == 1;
     }
     int maxc = cnt;
@@ -587,8 +587,8 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
   if (n <= 0) return;
   (void)hipMemsetAsync(w.hdr, 0, sizeof(GtHdr), s);
   k_gt_plan<<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan, w.hdr,
-                                                            w.terms, w.chunk_req);
-  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.chunk_req, w.plan, w.hdr, w.partial, y);
+                                                            w.terms, w.chunk_req, w.chunk);
+  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.chunk_req, w.plan, w.hdr, w.chunk, w.partial, y);
   k_gt_combine<<<n, 64, 0, s>>>(n, codes, w.plan, w.partial, y);
 }
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {

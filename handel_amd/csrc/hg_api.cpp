@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -431,9 +432,18 @@ static int build_gt_locked(hg_ctx* c, hipStream_t s) {
 
 // GT fold workspaces for n requests: a request's folded mask has at most
 // 4 nonzero 16-bit windows per registry-aligned 64-bit word, plus the block term
+// fold schedule: terms per chunk and k_gt_chunks workgroups (HG_GT_CHUNK /
+// HG_GT_GRID override them for tuning runs)
+static int env_int(const char* name, int def, int lo, int hi) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : def;
+  return v >= lo && v <= hi ? v : def;
+}
 static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
+  static const int chunk = env_int("HG_GT_CHUNK", kGtChunk, 1, 64);
+  static const int grid = env_int("HG_GT_GRID", 4096, 64, 65536);
   const size_t mmax = 4 * ((c->nreg + 15 + 63) / 64 + 1) + 1;  // nonzero 16-bit windows + the block term
-  const size_t cmax = (mmax + kGtChunk - 1) / kGtChunk;
+  const size_t cmax = (mmax + chunk - 1) / chunk;
   HG_CHECK(c, c->gt_plan.ensure(n));
   HG_CHECK(c, c->gt_hdr.ensure(1));
   HG_CHECK(c, c->gt_terms.ensure(n * mmax));
@@ -445,7 +455,8 @@ static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
   w.terms = c->gt_terms.p;
   w.chunk_req = c->gt_chunk_req.p;
   w.partial = c->gt_partial.p;
-  w.chunk_grid = 2048;
+  w.chunk_grid = grid;
+  w.chunk = chunk;
   return HG_OK;
 }
 

@@ -29,6 +29,10 @@ class BatchVerifier:
         if codes.any():
             raise ValueError(f"registry key {int(np.flatnonzero(codes)[0])} fails to unmarshal")
         self.hash_rc = eng.set_message(msg)
+        if self.hash_rc == 0:
+            # the GT tables of aggregate verification for this message and
+            # registry, now rather than in the first batch
+            eng.prepare_aggregate()
         self.node_id = node_id
 
     def _pack(self, items):

@@ -182,3 +182,46 @@ def test_sig_edge_cases_on_gt_path(engine):
     want = _oracle(msg, reg, reqs, words, bytes(sigs))
     assert list(codes) == list(want)
     assert list(codes[:5]) == [0, 0, 0, 0, 0] and codes[6] == 1
+
+
+@pytest.mark.parametrize("n_reg", [1, 2, 15, 17, 33, 100])
+def test_gt_small_and_ragged_registries(engine, n_reg):
+    """Registries that end inside a 16-key window (absent keys are 1 in the
+    window table) and inside a block (clipped top blocks), down to a single
+    key: every Handel level range of several nodes, plus level errors."""
+    rng = np.random.default_rng(n_reg)
+    ks = F.scalars(n_reg, seed=b"gt-small-%d" % n_reg)
+    reg = R.g2_scalar_base(F.scalar_bytes(ks))
+    assert list(engine.registry_load(reg)) == [0] * n_reg
+    msg = F.TEST_MESSAGES[1]
+    assert engine.set_message(msg) == 0
+    nodes = sorted({0, n_reg - 1, n_reg // 2})
+    ranges = _levels(n_reg, nodes) if n_reg > 1 else [(0, 1)]
+    reqs, words, sigs = _batch(ks, n_reg, msg, ranges, rng, tamper_every=3)
+    # one request past the registry end and one with bitlen != level size
+    bad = np.array([(max(0, n_reg - 1), 2, 2, 0), (0, 1, 2, 0)], dtype=REQ_DTYPE)
+    reqs = np.concatenate([reqs, bad])
+    sigs = sigs + sigs[:64] * 2
+    codes = engine.verify_aggregate(reqs, words, sigs)
+    assert list(codes) == list(_oracle(msg, reg, reqs, words, sigs))
+    assert list(codes[-2:]) == [3, 3]
+
+
+def test_registry_above_gt_limit_uses_g2_fold(engine):
+    """Registries above 16384 keys (GT tables > 32 GB) are verified by the G2
+    fold + two-pairing check; hg_prepare_aggregate has nothing to build."""
+    import bench
+
+    n_reg = 16385
+    kb = bench.seeded_scalars(n_reg, 99)
+    reg = engine.keygen(kb)
+    assert not engine.registry_load(reg).any()
+    assert engine.set_message(F.LIB_MESSAGE) == 0
+    assert engine.prepare_aggregate() == 0
+    scal = [int.from_bytes(kb[32 * i:32 * i + 32], "big") for i in range(n_reg)]
+    ranges = [(16376, 9), (0, 16), (8192, 8192), (16384, 1)]
+    rng = np.random.default_rng(8)
+    reqs, words, sigs = _batch(scal, n_reg, F.LIB_MESSAGE, ranges, rng, tamper_every=2)
+    codes = engine.verify_aggregate(reqs, words, sigs)
+    assert list(codes) == list(_oracle(F.LIB_MESSAGE, reg, reqs, words, sigs))
+    assert list(codes) == [1, 0, 1, 0]
