@@ -175,6 +175,8 @@ func (e *Engine) SetMessage(msg []byte) error {
 // aggregate verification for it and the loaded registry now (e(H, pk_i) and
 // the GT window/block products: ≈ 15 ms for 4000 keys) instead of in the
 // first aggregate call. Call it once per Handel run after LoadRegistry.
+// Without it the engine builds the tables by request volume (see
+// AggregateTables).
 func (e *Engine) PrepareAggregate(msg []byte) error {
 	if err := e.SetMessage(msg); err != nil {
 		return err
@@ -187,6 +189,14 @@ func (e *Engine) PrepareAggregate(msg []byte) error {
 	default:
 		return e.fail(rc)
 	}
+}
+
+// AggregateTables reports the table level aggregate checks run at: 0 = G2
+// key fold + two pairings (a message's first 16384 requests), 1 = GT fold over
+// 8-key windows, 2 = over 16-key windows (after PrepareAggregate, or 2^20
+// requests).
+func (e *Engine) AggregateTables() int {
+	return int(C.hg_aggregate_tables(e.ctx))
 }
 
 // VerifyBatch runs n = len(sigs)/64 independent PublicKey.VerifySignature(msg,

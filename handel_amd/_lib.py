@@ -54,6 +54,7 @@ SIGNATURES = {
     "hg_registry_load": (_I, [_P, _P, _SZ, _P]),
     "hg_registry_size": (_SZ, [_P]),
     "hg_prepare_aggregate": (_I, [_P]),
+    "hg_aggregate_tables": (_I, [_P]),
     "hg_set_message": (_I, [_P, _P, _SZ]),
     "hg_verify_batch": (_I, [_P, _P, _P, _SZ, _P]),
     "hg_verify_batch_msg": (_I, [_P, _P, _SZ, _P, _P, _SZ, _P]),

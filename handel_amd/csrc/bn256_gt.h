@@ -10,9 +10,9 @@ struct Gt {
   uint32_t w[120];
 };
 static constexpr int kGtChunk = 8;  // default window-table values per fold chunk (one team)
-// The fold's windows: aligned 16-key windows, 65536 subset products each
-// (7.9 GB of HBM for a 4000-key registry; built from the 8-key tables)
-static constexpr int kGtWinBits = 16;
+// The fold's windows: aligned 8-key windows (256 subset products each, 61 MB
+// for a 4000-key registry) or 16-key windows (65536 each, 7.9 GB, built from
+// the 8-key tables): GtWork.win_bits
 
 // per-request fold plan (k_gt_plan, k_gt_scan)
 struct GtReq {
@@ -27,7 +27,7 @@ struct GtHdr {
   int terms, chunks;
 };
 // level k >= 4 block j of the registry at blk[base[k] + j] (levels <= 3 are
-// window-table entries)
+// entries of the window table in use)
 struct GtBlockIndex {
   int base[24];
 };
@@ -40,13 +40,15 @@ struct GtWork {
   Gt* partial;
   int chunk_grid;  // workgroups of k_gt_chunks (4 teams each)
   int chunk;       // terms per chunk
+  int win_bits;    // 8 or 16: which window table `win` is
 };
 
 // G_i = e(H, pk_i) for the n registry keys
 void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s);
-// w8[256 w + s] = product of G_{8w + j} over the bits j of s (absent keys = 1);
-// then w16[65536 w + s] = product of G_{16w + j} over the bits j of s
-void launch_gt_windows(const Gt* key, int nreg, Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s);
+// w8[256 w + s] = product of G_{8w + j} over the bits j of s (absent keys = 1)
+void launch_gt_windows8(const Gt* key, int nreg, Gt* w8, int nwin8, hipStream_t s);
+// w16[65536 w + s] = product of G_{16w + j} over the bits j of s, from w8
+void launch_gt_windows16(const Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s);
 // dst[j] = src[2j] * src[2j + 1] (entries `stride` apart; a missing odd entry = 1)
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s);
 // the fold of n requests: y[r] = conj(e(H, aggregate key of r)); codes: level

@@ -276,10 +276,18 @@ HG_DEV const Gt* term_ptr(uint32_t t, const Gt* win, const Gt* blk) {
 // registry-aligned windows, and the owner of each chunk. An empty bitset is
 // the reference's nil-aggregate panic (HG_ERR_EMPTY_AGG).
 static constexpr int kPlanWaves = 16;  // requests per k_gt_plan workgroup (one wave each)
+template <int W>
+HG_DEV uint32_t nz_units(uint64_t x) {
+  return W == 8 ? nz_bytes(x) : nz_halves(x);
+}
+// W: registry-aligned window width of the fold's table (8: the 256-entry
+// tables, 16: the 65536-entry ones)
+template <int W>
 __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* reqs, int n, const uint64_t* words,
                                                              int32_t* codes, int nreg, int levels, GtBlockIndex bi,
                                                              GtReq* plan, GtHdr* hdr, uint32_t* terms,
                                                              int* chunk_req, int chunk) {
+  constexpr uint32_t kUnits = 64 / W, kMask = (1u << W) - 1u, kShift = W == 8 ? 3 : 4;
   __shared__ int sm[kPlanWaves], sc[kPlanWaves], base_m, base_c;
   const int wv = threadIdx.x >> 6;
   const int r = blockIdx.x * kPlanWaves + wv;
@@ -293,9 +301,9 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
     q = reqs[r];
     uint32_t cnt = 0, nzs = 0, nzu = 0;
     for (uint32_t wi = lane; wi < (q.bitlen + 63) / 64; wi += 64) cnt += __popcll(agg_word(q, words, wi));
-    for (uint32_t v = lane; v < agg_nrwords_w<kGtWinBits>(q); v += 64) {
-      nzs += nz_halves(agg_rword_w<kGtWinBits>(q, words, (int)v, false));
-      nzu += nz_halves(agg_rword_w<kGtWinBits>(q, words, (int)v, true));
+    for (uint32_t v = lane; v < agg_nrwords_w<W>(q); v += 64) {
+      nzs += nz_units<W>(agg_rword_w<W>(q, words, (int)v, false));
+      nzu += nz_units<W>(agg_rword_w<W>(q, words, (int)v, true));
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
@@ -341,9 +349,9 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
   if (g.comp) {
     if (lane == 0) {
       uint32_t t;
-      if (g.k <= 4) {  // a block inside one window: that window's subset entry
-        const uint32_t mask = ((1u << (1u << g.k)) - 1u) << (q.offset & 15u);
-        t = (q.offset >> 4) * 65536u + (mask & 0xffffu);
+      if (g.k <= 3) {  // a block inside one 8-key window: that window's subset entry
+        const uint32_t mask = ((1u << (1u << g.k)) - 1u) << (q.offset & (uint32_t)(W - 1));
+        t = (q.offset >> kShift) * (kMask + 1u) + (mask & kMask);
       } else {
         t = kTermBlk | (uint32_t)(bi.base[g.k] + (q.offset >> g.k));
       }
@@ -351,13 +359,13 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
     }
     at++;
   }
-  const uint32_t nrw = agg_nrwords_w<kGtWinBits>(q);
-  const uint32_t win0 = q.offset >> 4;
+  const uint32_t nrw = agg_nrwords_w<W>(q);
+  const uint32_t win0 = q.offset >> kShift;
   const uint32_t flag = g.comp ? 0u : kTermConj;
   for (uint32_t v0 = 0; v0 < nrw; v0 += 64) {
     const uint32_t v = v0 + lane;
-    const uint64_t mb = v < nrw ? agg_rword_w<kGtWinBits>(q, words, (int)v, g.comp != 0) : 0;
-    const uint32_t pc = nz_halves(mb);
+    const uint64_t mb = v < nrw ? agg_rword_w<W>(q, words, (int)v, g.comp != 0) : 0;
+    const uint32_t pc = nz_units<W>(mb);
     uint32_t inc = pc;  // inclusive prefix over the wave
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -366,9 +374,9 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
     }
     uint32_t pos = at + inc - pc;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t half = (uint32_t)(mb >> (16 * j)) & 0xffffu;
-      if (half) terms[pos++] = ((win0 + 4 * v + j) * 65536u + half) | flag;
+    for (uint32_t j = 0; j < kUnits; j++) {
+      const uint32_t unit = (uint32_t)(mb >> (W * j)) & kMask;
+      if (unit) terms[pos++] = ((win0 + kUnits * v + j) * (kMask + 1u) + unit) | flag;
     }
     at += __shfl(inc, 63);
   }
@@ -573,11 +581,13 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, int n, c
 void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s) {
   if (n > 0) k_gt_keys<4><<<nblk(n, 4), 64, 0, s>>>(reg, n, tab, h, out);
 }
-void launch_gt_windows(const Gt* key, int nreg, Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s) {
+void launch_gt_windows8(const Gt* key, int nreg, Gt* w8, int nwin8, hipStream_t s) {
   if (nwin8 <= 0) return;
   k_gt_nib<<<nblk(2 * nwin8, 4), 64, 0, s>>>(key, nreg, nwin8, w8);
   k_gt_cross<<<nblk(15 * nwin8, 4), 64, 0, s>>>(nwin8, w8);
-  k_gt_win16<<<nblk(256 * nwin16, 4), 64, 0, s>>>(w8, nwin8, nwin16, w16);
+}
+void launch_gt_windows16(const Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s) {
+  if (nwin16 > 0) k_gt_win16<<<nblk(256 * nwin16, 4), 64, 0, s>>>(w8, nwin8, nwin16, w16);
 }
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s) {
   if (ndst > 0) k_gt_blocks<<<nblk(ndst, 4), 64, 0, s>>>(src, stride, nsrc, dst, ndst);
@@ -586,8 +596,12 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
                     const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, hipStream_t s) {
   if (n <= 0) return;
   (void)hipMemsetAsync(w.hdr, 0, sizeof(GtHdr), s);
-  k_gt_plan<<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan, w.hdr,
-                                                            w.terms, w.chunk_req, w.chunk);
+  if (w.win_bits == 16)
+    k_gt_plan<16><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
+                                                                  w.hdr, w.terms, w.chunk_req, w.chunk);
+  else
+    k_gt_plan<8><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
+                                                                 w.hdr, w.terms, w.chunk_req, w.chunk);
   k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.chunk_req, w.plan, w.hdr, w.chunk, w.partial, y);
   k_gt_combine<<<n, 64, 0, s>>>(n, codes, w.plan, w.partial, y);
 }

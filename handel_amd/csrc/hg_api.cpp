@@ -178,7 +178,11 @@ struct hg_ctx {
   // GT path of aggregate verification (bn256_gt.hip): e(H, pk_i), window
   // subset products and block products, valid for the current message and
   // registry (rebuilt by the first aggregate submission after either changes)
-  bool gt_ready = false;
+  // 0: none (aggregates use the G2 fold); 1: e(H, pk_i), 8-key windows and
+  // blocks; 2: + 16-key windows. Reset by a message or registry change;
+  // raised by hg_prepare_aggregate or by request volume (gt_requests).
+  int gt_level = 0;
+  size_t gt_requests = 0;
   DevBuf<Gt> gt_key, gt_w8, gt_win, gt_blk;  // gt_w8: 8-key windows, gt_win: 16-key windows
   GtBlockIndex gt_bi{};
   // GT fold workspaces
@@ -294,7 +298,7 @@ static void release_all(hg_ctx* c) {
   c->gt_chunk_req.release();
   c->gt_partial.release();
   c->gt_y.release();
-  c->gt_ready = false;
+  c->gt_level = 0;
   for (auto& ph : c->events) {
     for (auto& pr : ph) {
       (void)hipEventDestroy(pr.first);
@@ -323,7 +327,8 @@ static int set_message_locked(hg_ctx* c, const uint8_t* msg, size_t len) {
   sha256(msg, len, d);
   uint32_t k[8];
   c->has_msg = false;
-  c->gt_ready = false;  // the GT tables are e(H, .) of the previous message
+  c->gt_level = 0;  // the GT tables are e(H, .) of the previous message
+  c->gt_requests = 0;
   c->msg.assign(msg, msg + len);
   c->hash_eof = !hash_scalar(d, k);
   if (c->hash_eof) {
@@ -386,48 +391,80 @@ static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector
   }
 }
 
-// The GT tables take ~1.97 MB of HBM per registry key (16-key windows of
-// 65536 GT values): registries up to 16384 keys (32 GB) use the GT path,
-// larger ones the G2 point fold.
+// The GT tables. Level 1 (e(H, pk_i) for every key, 8-key window subset
+// products, aligned block products: ≈ 3 ms and 61 MB for 4000 keys) saves
+// ≈ 0.6 ms per 4096-request batch against the G2 fold (config 3), so it pays
+// for itself after ≈ 20 k requests of one message; level 2 (16-key windows:
+// ≈ 12.5 ms more and ≈ 1.97 MB of HBM per key, registries up to 16384 keys)
+// saves another ≈ 0.05 ms per batch and pays off after ≈ 1 M requests. The
+// thresholds are those break-even volumes (a rent-or-buy rule: at most about
+// twice the cost of the better choice in hindsight). A message or registry
+// change drops the tables and restarts the count. hg_prepare_aggregate builds
+// the top level at once (serving). HG_GT_LEVEL=0/1/2 pins a level (0 = G2
+// fold only; tests and A/B runs); HG_AGG_PATH=g2 = 0.
 static constexpr size_t kGtMaxRegistry = 16384;
-// Which fold verifies aggregate requests: the GT path (bn256_gt.hip, default)
-// or the G2 point fold + k_verify (HG_AGG_PATH=g2, kept for A/B runs).
-static bool gt_path_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("HG_AGG_PATH");
-    return !(e && strcmp(e, "g2") == 0);
+static constexpr size_t kGtLevel1Requests = 16384;
+static constexpr size_t kGtLevel2Requests = (size_t)1 << 20;
+static int gt_forced_level() {
+  static const int lvl = [] {
+    const char* p = getenv("HG_AGG_PATH");
+    if (p && strcmp(p, "g2") == 0) return 0;
+    const char* e = getenv("HG_GT_LEVEL");
+    if (!e) return -1;
+    const int v = atoi(e);
+    return v >= 0 && v <= 2 ? v : -1;
   }();
-  return on;
+  return lvl;
 }
+static int gt_max_level(const hg_ctx* c) { return c->nreg <= kGtMaxRegistry ? 2 : 1; }
 
-// e(H, pk_i), the window subset products and the block products of levels
-// k >= 4 (levels <= 3 are window entries) for the current message and
-// registry, on stream s (inside a submission).
-static int build_gt_locked(hg_ctx* c, hipStream_t s) {
+// builds the tables up to `level` on stream s (inside a submission)
+static int build_gt_locked(hg_ctx* c, hipStream_t s, int level) {
   const int n = (int)c->nreg;
   const int nwin8 = (n + 7) / 8, nwin16 = (n + 15) / 16;
-  HG_CHECK(c, c->gt_key.ensure(n));
-  HG_CHECK(c, c->gt_w8.ensure((size_t)nwin8 * 256));
-  HG_CHECK(c, c->gt_win.ensure((size_t)nwin16 * 65536));
-  // blocks of level k >= 5 (levels <= 4 are 16-key window entries)
-  int cnt[24] = {0};
-  int total = 0;
-  for (int k = 5; k <= c->block_levels && k < 24; k++) {
-    cnt[k] = (int)(((size_t)n + ((size_t)1 << k) - 1) >> k);
-    c->gt_bi.base[k] = total;
-    total += cnt[k];
+  if (c->gt_level < 1 && level >= 1) {
+    HG_CHECK(c, c->gt_key.ensure(n));
+    HG_CHECK(c, c->gt_w8.ensure((size_t)nwin8 * 256));
+    // blocks of level k >= 4 (levels <= 3 are window entries)
+    int cnt[24] = {0};
+    int total = 0;
+    for (int k = 4; k <= c->block_levels && k < 24; k++) {
+      cnt[k] = (int)(((size_t)n + ((size_t)1 << k) - 1) >> k);
+      c->gt_bi.base[k] = total;
+      total += cnt[k];
+    }
+    if (total) HG_CHECK(c, c->gt_blk.ensure(total));
+    launch_gt_keys(c->reg.p, n, c->d_lines, c->d_h, c->gt_key.p, s);
+    launch_gt_windows8(c->gt_key.p, n, c->gt_w8.p, nwin8, s);
+    for (int k = 4; k <= c->block_levels && k < 24; k++) {
+      if (k == 4) launch_gt_blocks(c->gt_w8.p + 255, 256, nwin8, c->gt_blk.p + c->gt_bi.base[4], cnt[4], s);
+      else launch_gt_blocks(c->gt_blk.p + c->gt_bi.base[k - 1], 1, cnt[k - 1], c->gt_blk.p + c->gt_bi.base[k], cnt[k], s);
+    }
+    int rc = check_launch(c);
+    if (rc) return rc;
+    c->gt_level = 1;
   }
-  if (total) HG_CHECK(c, c->gt_blk.ensure(total));
-  launch_gt_keys(c->reg.p, n, c->d_lines, c->d_h, c->gt_key.p, s);
-  launch_gt_windows(c->gt_key.p, n, c->gt_w8.p, nwin8, c->gt_win.p, nwin16, s);
-  for (int k = 5; k <= c->block_levels && k < 24; k++) {
-    if (k == 5) launch_gt_blocks(c->gt_win.p + 0xffff, 65536, nwin16, c->gt_blk.p + c->gt_bi.base[5], cnt[5], s);
-    else launch_gt_blocks(c->gt_blk.p + c->gt_bi.base[k - 1], 1, cnt[k - 1], c->gt_blk.p + c->gt_bi.base[k], cnt[k], s);
+  if (c->gt_level < 2 && level >= 2) {
+    HG_CHECK(c, c->gt_win.ensure((size_t)nwin16 * 65536));
+    launch_gt_windows16(c->gt_w8.p, nwin8, c->gt_win.p, nwin16, s);
+    int rc = check_launch(c);
+    if (rc) return rc;
+    c->gt_level = 2;
   }
-  int rc = check_launch(c);
-  if (rc) return rc;
-  c->gt_ready = true;
   return HG_OK;
+}
+
+// the table level an aggregate submission of n requests runs at (counting
+// them towards the volume policy)
+static int gt_submission_level(hg_ctx* c, size_t n) {
+  if (c->hash_eof || c->nreg == 0) return 0;
+  const int forced = gt_forced_level();
+  const int top = gt_max_level(c);
+  if (forced >= 0) return forced < top ? forced : top;
+  c->gt_requests += n;
+  int want = c->gt_requests >= kGtLevel2Requests ? 2 : (c->gt_requests >= kGtLevel1Requests ? 1 : 0);
+  if (want < c->gt_level) want = c->gt_level;
+  return want < top ? want : top;
 }
 
 // GT fold workspaces for n requests: a request's folded mask has at most
@@ -442,7 +479,7 @@ static int env_int(const char* name, int def, int lo, int hi) {
 static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
   static const int chunk = env_int("HG_GT_CHUNK", kGtChunk, 1, 64);
   static const int grid = env_int("HG_GT_GRID", 4096, 64, 65536);
-  const size_t mmax = 4 * ((c->nreg + 15 + 63) / 64 + 1) + 1;  // nonzero 16-bit windows + the block term
+  const size_t mmax = 8 * ((c->nreg + 7 + 63) / 64 + 1) + 1;  // nonzero 8-key windows + the block term
   const size_t cmax = (mmax + chunk - 1) / chunk;
   HG_CHECK(c, c->gt_plan.ensure(n));
   HG_CHECK(c, c->gt_hdr.ensure(1));
@@ -471,7 +508,8 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   }
   // GT path: the verdict needs no aggregate key in G2; the G2 fold still runs
   // when the caller wants the aggregate keys' marshals
-  const bool use_gt = verify && gt_path_enabled() && !c->hash_eof && c->nreg > 0 && c->nreg <= kGtMaxRegistry;
+  const int level = verify ? gt_submission_level(c, n) : 0;
+  const bool use_gt = level > 0;
   const bool g2_fold = !use_gt || d_agg;
   GtWork gw{};
   if (use_gt) {
@@ -489,18 +527,19 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     HG_CHECK(c, c->codes_b.ensure(n));
   }
   HG_CHECK(c, begin(c, s));
-  if (use_gt && !c->gt_ready) {
-    int rc = build_gt_locked(c, s);
+  if (use_gt && c->gt_level < level) {
+    int rc = build_gt_locked(c, s, level);
     if (rc) return rc;
   }
+  gw.win_bits = level == 2 ? 16 : 8;
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
   PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
   if (g2_fold)
     launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
                      d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
   if (use_gt)
-    launch_gt_fold(d_reqs, (int)n, d_words, d_lvl, (int)c->nreg, c->block_levels, c->gt_win.p, c->gt_blk.p,
-                   c->gt_bi, gw, c->gt_y.p, s);
+    launch_gt_fold(d_reqs, (int)n, d_words, d_lvl, (int)c->nreg, c->block_levels,
+                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, s);
   fold.stop();
   if (d_agg) {
     launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);
@@ -693,7 +732,8 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   // leaves it empty (every aggregate request then fails its range check)
   c->nreg = 0;
   c->block_levels = 0;
-  c->gt_ready = false;
+  c->gt_level = 0;
+  c->gt_requests = 0;
   HG_CHECK(c, begin(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   HG_CHECK(c, c->reg.ensure(n));
@@ -754,16 +794,24 @@ int hg_prepare_aggregate(hg_ctx* c) {
     c->err = "hg_prepare_aggregate: needs a message and a registry";
     return HG_ERR_ARG;
   }
-  if (c->nreg > kGtMaxRegistry || !gt_path_enabled()) return HG_OK;  // aggregates use the G2 fold
   if (c->hash_eof) return HG_ERR_HASH_EOF;
-  if (c->gt_ready) return HG_OK;
+  const int forced = gt_forced_level();
+  int level = gt_max_level(c);
+  if (forced >= 0 && forced < level) level = forced;
+  if (c->gt_level >= level) return HG_OK;
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, begin(c, c->stream));
-  int rc = build_gt_locked(c, c->stream);
+  int rc = build_gt_locked(c, c->stream, level);
   if (rc) return rc;
   HG_CHECK(c, end(c, c->stream));
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
+}
+
+int hg_aggregate_tables(hg_ctx* c) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  return c->gt_level;
 }
 
 size_t hg_registry_size(hg_ctx* c) {

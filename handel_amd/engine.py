@@ -89,6 +89,11 @@ class Engine:
         return self._check(self.L.hg_prepare_aggregate(self.ctx), "hg_prepare_aggregate",
                            ok=(0, _lib.HG_ERR_HASH_EOF))
 
+    def aggregate_tables(self) -> int:
+        """Table level aggregate requests run at (hg_aggregate_tables): 0 = G2
+        fold, 1 = GT fold over 8-key windows, 2 = over 16-key windows."""
+        return int(self.L.hg_aggregate_tables(self.ctx))
+
     def registry_load(self, pks: bytes) -> np.ndarray:
         a = _u8(pks)
         n = len(a) // 128

@@ -7,6 +7,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Aggregate requests in the GPU suite run on the headline path (GT fold over
+# 16-key windows) whatever their volume; tests of the other table levels and
+# of the volume policy run in child processes with their own HG_GT_LEVEL.
+os.environ.setdefault("HG_GT_LEVEL", "2")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")

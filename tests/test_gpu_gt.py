@@ -104,12 +104,8 @@ def test_tables_follow_message_and_registry(engine):
                     assert (np.asarray(codes) == 0).sum() == 0
 
 
-def test_gt_and_g2_paths_agree():
-    """The GT path (this process) and the G2 point fold + two-pairing check
-    (HG_AGG_PATH=g2, a child process) give the oracle's verdicts on the same
-    batch: 1024 multisigs at random Handel levels of a 1000-key registry."""
-    code = r"""
-import json, sys
+_CHILD = r"""
+import json, os, sys
 import numpy as np
 sys.path.insert(0, %r)
 import bench
@@ -117,15 +113,30 @@ from handel_amd.engine import Engine
 e = Engine(device=0, flavor="go")
 assert e.set_message(bench.LIB_MESSAGE) == 0
 reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(e, 1000, 1024, seed=5)
-print(json.dumps([int(c) for c in e.verify_aggregate(reqs, words, sigs)]))
+codes = e.verify_aggregate(reqs, words, sigs)
+print(json.dumps({"codes": [int(c) for c in codes], "level": e.aggregate_tables()}))
 """ % ROOT
+
+
+def _child(env_over, code=_CHILD):
+    env = {k: v for k, v in os.environ.items() if k not in ("HG_GT_LEVEL", "HG_AGG_PATH")}
+    env.update(env_over)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_gt_and_g2_paths_agree():
+    """Every table level gives the oracle's verdicts on the same batch (1024
+    multisigs at random Handel levels of a 1000-key registry): the GT fold over
+    16-key windows (HG_GT_LEVEL=2), over 8-key windows (1), the G2 point fold
+    + two-pairing check (0, and HG_AGG_PATH=g2) — each in a child process."""
     outs = {}
-    for path in ("gt", "g2"):
-        env = dict(os.environ, HG_AGG_PATH=path)
-        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stderr[-2000:]
-        outs[path] = json.loads(r.stdout.strip().splitlines()[-1])
-    assert outs["gt"] == outs["g2"]
+    for name, env in (("gt16", {"HG_GT_LEVEL": "2"}), ("gt8", {"HG_GT_LEVEL": "1"}),
+                      ("g2", {"HG_GT_LEVEL": "0"}), ("g2env", {"HG_AGG_PATH": "g2"})):
+        outs[name] = _child(env)
+    assert [outs[k]["level"] for k in ("gt16", "gt8", "g2", "g2env")] == [2, 1, 0, 0]
+    assert outs["gt16"]["codes"] == outs["gt8"]["codes"] == outs["g2"]["codes"] == outs["g2env"]["codes"]
     import bench
     from handel_amd.engine import Engine
 
@@ -135,8 +146,45 @@ print(json.dumps([int(c) for c in e.verify_aggregate(reqs, words, sigs)]))
         reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(e, 1000, 1024, seed=5)
     finally:
         e.close()
-    assert outs["gt"] == [int(c) for c in expect]
-    assert outs["gt"] == [int(c) for c in _oracle(bench.LIB_MESSAGE, reg, reqs, words, sigs)]
+    assert outs["gt16"]["codes"] == [int(c) for c in expect]
+    assert outs["gt16"]["codes"] == [int(c) for c in _oracle(bench.LIB_MESSAGE, reg, reqs, words, sigs)]
+
+
+def test_volume_policy():
+    """Without HG_GT_LEVEL: a message's first requests use the G2 fold, the
+    8-key GT tables appear once 16384 requests have come in, a new message
+    drops them, hg_prepare_aggregate builds the 16-key level — and the
+    verdicts are the same at every step."""
+    code = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, %r)
+import bench
+from handel_amd.engine import Engine
+e = Engine(device=0, flavor="go")
+assert e.set_message(bench.LIB_MESSAGE) == 0
+reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(e, 500, 3000, seed=9)
+out = []
+def run(a, b):
+    c = e.verify_aggregate(reqs[a:b], words, sigs[64 * a:64 * b])
+    out.append((bool(np.array_equal(c, expect[a:b])), e.aggregate_tables()))
+run(0, 1000)
+for _ in range(5):
+    run(0, 3000)         # 16000 requests so far: still the G2 fold
+run(1000, 2000)          # 17000: the 8-key tables
+assert e.set_message(b"Peaches and Cream") == 0
+assert e.set_message(bench.LIB_MESSAGE) == 0
+run(0, 100)              # tables dropped with the message change
+assert e.prepare_aggregate() == 0
+run(0, 3000)
+print(json.dumps(out))
+""" % ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("HG_GT_LEVEL", "HG_AGG_PATH")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert [ok for ok, _ in out] == [True] * 9
+    assert [lvl for _, lvl in out] == [0] * 6 + [1, 0, 2]
 
 
 def test_sig_edge_cases_on_gt_path(engine):
@@ -207,9 +255,10 @@ def test_gt_small_and_ragged_registries(engine, n_reg):
     assert list(codes[-2:]) == [3, 3]
 
 
-def test_registry_above_gt_limit_uses_g2_fold(engine):
-    """Registries above 16384 keys (GT tables > 32 GB) are verified by the G2
-    fold + two-pairing check; hg_prepare_aggregate has nothing to build."""
+def test_registry_above_16key_limit_uses_8key_tables(engine):
+    """Registries above 16384 keys (16-key tables > 32 GB) stop at the 8-key
+    GT tables: hg_prepare_aggregate builds level 1, and verdicts over the
+    ragged last window (key 16384) and a full half match the oracle."""
     import bench
 
     n_reg = 16385
@@ -218,6 +267,7 @@ def test_registry_above_gt_limit_uses_g2_fold(engine):
     assert not engine.registry_load(reg).any()
     assert engine.set_message(F.LIB_MESSAGE) == 0
     assert engine.prepare_aggregate() == 0
+    assert engine.aggregate_tables() == 1
     scal = [int.from_bytes(kb[32 * i:32 * i + 32], "big") for i in range(n_reg)]
     ranges = [(16376, 9), (0, 16), (8192, 8192), (16384, 1)]
     rng = np.random.default_rng(8)
