@@ -52,9 +52,11 @@ void launch_gt_windows16(const Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream
 // dst[j] = src[2j] * src[2j + 1] (entries `stride` apart; a missing odd entry = 1)
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s);
 // the fold of n requests: y[r] = conj(e(H, aggregate key of r)); codes: level
-// codes in, HG_ERR_EMPTY_AGG added for empty bitsets
+// codes in, HG_ERR_EMPTY_AGG added for empty bitsets; zero_hdr: clear the
+// range counters first (false: the caller's prologue did)
 void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_t* codes, int nreg, int levels,
-                    const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, hipStream_t s);
+                    const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, bool zero_hdr,
+                    hipStream_t s);
 // FE(Miller(G2Base at -sig_r)) == y[r] for every request still HG_OK
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s);
 

@@ -413,26 +413,37 @@ __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, 
     int maxc = cnt;
 #pragma unroll
     for (int d = 16; d < 64; d <<= 1) maxc = max(maxc, __shfl_xor(maxc, d));
-    Fp cur, nxt, one;
+    // the chunk's term words, read once: lane tl of the team holds term tl
+    // (terms past 16 are read from the list), so no table read waits on a
+    // dependent index load
+    const uint32_t my_t = T.tl < cnt ? terms[first + T.tl] : 0u;
+    const int tbase = threadIdx.x & 48;
+    auto term = [&](int i) -> uint32_t {  // wave-uniform i: every lane runs the shuffle
+      const uint32_t v = (uint32_t)__shfl((int)my_t, tbase + (i & 15), 64);
+      return i < 16 ? v : (i < cnt ? terms[first + i] : 0u);
+    };
+    Fp cur, n1, n2, one;
     gt_one_value(one, T);
-    fp_zero(nxt);
-    uint32_t t0 = valid ? terms[first] : 0u, t1 = 0u;
-    gt_read(cur, term_ptr(t0, win, blk), T);
+    fp_zero(n1);
+    fp_zero(n2);
+    const uint32_t t0 = term(0);
+    gt_read(cur, term_ptr(valid ? t0 : 0u, win, blk), T);
     fp_sel(cur, valid, cur, one);
-    gt_put(T, S_A, cur, (t0 & kTermConj) != 0);
-    if (1 < cnt) {
-      t1 = terms[first + 1];
-      gt_read(nxt, term_ptr(t1, win, blk), T);
-    }
+    gt_put(T, S_A, cur, valid && (t0 & kTermConj) != 0);
+    // two table values in flight across the products (a read of the 16-key
+    // table is a fresh HBM page most of the time)
+    uint32_t t1 = term(1), t2 = term(2);
+    if (1 < cnt) gt_read(n1, term_ptr(t1, win, blk), T);
+    if (2 < cnt) gt_read(n2, term_ptr(t2, win, blk), T);
 #pragma unroll 1
     for (int i = 1; i < maxc; i++) {
       Fp v;
-      fp_sel(v, i < cnt, nxt, one);
+      fp_sel(v, i < cnt, n1, one);
       gt_put(T, S_B, v, i < cnt && (t1 & kTermConj) != 0);
-      if (i + 1 < cnt) {  // in flight across the product
-        t1 = terms[first + i + 1];
-        gt_read(nxt, term_ptr(t1, win, blk), T);
-      }
+      n1 = n2;
+      t1 = t2;
+      t2 = term(i + 2);
+      if (i + 2 < cnt) gt_read(n2, term_ptr(t2, win, blk), T);
       fold_mul(T, S);
     }
     team_sync();
@@ -456,10 +467,19 @@ __global__ __launch_bounds__(64) void k_gt_combine(int n, const int32_t* codes, 
   XStream S = x_stream();
   const int rounds = (g.chunks + 3) / 4;
   gt_load_or_one(T, S_A, partial + (team < g.chunks ? g.chunk_off + team : 0), team < g.chunks);
+  // the team's next partial in flight across the product
+  Fp one, nx;
+  gt_one_value(one, T);
+  nx = one;
+  int c = team + 4;
+  if (c < g.chunks) gt_read(nx, partial + g.chunk_off + c, T);
 #pragma unroll 1
   for (int i = 1; i < rounds; i++) {
-    const int c = team + 4 * i;
-    gt_load_or_one(T, S_B, partial + (c < g.chunks ? g.chunk_off + c : 0), c < g.chunks);
+    Fp v;
+    fp_sel(v, c < g.chunks, nx, one);
+    gt_put(T, S_B, v, false);
+    c += 4;
+    if (c < g.chunks) gt_read(nx, partial + g.chunk_off + c, T);
     fold_mul(T, S);
   }
   for (int d = 1; d < (g.chunks > 2 ? 4 : 2); d <<= 1) {
@@ -482,16 +502,28 @@ using ILfev = XInst<XP_LFEV, S_F, S_F>;
 using IFeval = XInst<XP_FEVAL>;
 using ILfix = XInst<XP_LINE_FIX, S_F, S_F>;
 
-// FBX, FCY of line s (the evaluation's inputs) / FA of line s
-HG_DEV void load_line_bc(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
-  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
-  if (T.tl >= 2 && T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
-  team_sync();
+// The G2Base lines reach the team's registers through one VGPR element per
+// lane (lane tl < 6 holds Fp tl of a line: a.x, a.y, bx.x, bx.y, cy.x, cy.y),
+// read from the table one publication ahead, so the L2 latency of the read
+// overlaps the rounds between (it used to be exposed twice per Miller step).
+struct LinePipe {
+  Fp c;
+};
+// fetch the part of line s that lanes [lo, hi) publish next
+HG_DEV void line_fetch(const Team& T, LinePipe& P, const LineCoef* tab, int s, int lo, int hi) {
+  if (T.tl >= lo && T.tl < hi) P.c = reinterpret_cast<const Fp*>(&tab[s])[T.tl];
 }
-HG_DEV void load_line_a(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
-  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
-  if (T.tl < 2) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
+// FBX, FCY of the held line (the evaluation's inputs), then the next line's
+// FBX, FCY into flight; FA likewise
+HG_DEV void publish_line_bc(const Team& T, uint32_t* F, LinePipe& P, const LineCoef* tab, int next) {
+  if (T.tl >= 2 && T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, P.c);
   team_sync();
+  if (next < kNumLines) line_fetch(T, P, tab, next, 2, 6);
+}
+HG_DEV void publish_line_a(const Team& T, uint32_t* F, LinePipe& P, const LineCoef* tab, int next) {
+  if (T.tl < 2) st_fp(F + (R_FA_x + T.tl) * 10, P.c);
+  team_sync();
+  if (next < kNumLines) line_fetch(T, P, tab, next, 0, 2);
 }
 HG_DEV void sig_unit_fix(const Team& T, uint32_t* F, bool use_s) {
   team_sync();
@@ -513,19 +545,22 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
     st_fp(F + R_NSY * 10, nsy);
   }
   team_sync();
+  LinePipe P;
+  fp_zero(P.c);
+  line_fetch(T, P, tab, 0, 0, 6);
   int s = 0;
   for (int i = kNafLen - 1; i > 0; i--) {
     const int d = naf[i - 1];
-    load_line_bc(T, F, tab, s);
-    load_line_a(T, F, tab, s);
+    publish_line_bc(T, F, P, tab, s + 1);
+    publish_line_a(T, F, P, tab, s + 1);
     // f^2 (f = 1 on the first digit) beside line s evaluated at -sig
     ISdbl::run(T, S, d != 0 ? xh<ILfev>() : xh<ILfix>());
     sig_unit_fix(T, F, use_s);
     const XHint after_digit = i > 1 ? xh<ISdbl>() : xh<IFeval>();
     if (d != 0) {
-      load_line_bc(T, F, tab, s + 1);  // read by the evaluation beside f * line s
+      publish_line_bc(T, F, P, tab, s + 2);  // read by the evaluation beside f * line s
       ILfev::run(T, S, xh<ILfix>());
-      load_line_a(T, F, tab, s + 1);
+      publish_line_a(T, F, P, tab, s + 2);
       sig_unit_fix(T, F, use_s);
       ILfix::run(T, S, after_digit);
       s += 2;
@@ -535,13 +570,13 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
     }
   }
   // the two Frobenius lines
-  load_line_bc(T, F, tab, s);
-  load_line_a(T, F, tab, s);
+  publish_line_bc(T, F, P, tab, s + 1);
+  publish_line_a(T, F, P, tab, s + 1);
   IFeval::run(T, S, xh<ILfev>());
   sig_unit_fix(T, F, use_s);
-  load_line_bc(T, F, tab, s + 1);
+  publish_line_bc(T, F, P, tab, kNumLines);
   ILfev::run(T, S, xh<ILfix>());
-  load_line_a(T, F, tab, s + 1);
+  publish_line_a(T, F, P, tab, kNumLines);
   sig_unit_fix(T, F, use_s);
   ILfix::run(T, S, after);
 }
@@ -593,9 +628,9 @@ void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hi
   if (ndst > 0) k_gt_blocks<<<nblk(ndst, 4), 64, 0, s>>>(src, stride, nsrc, dst, ndst);
 }
 void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_t* codes, int nreg, int levels,
-                    const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, hipStream_t s) {
+                    const Gt* win, const Gt* blk, const GtBlockIndex& bi, GtWork w, Gt* y, bool zero_hdr, hipStream_t s) {
   if (n <= 0) return;
-  (void)hipMemsetAsync(w.hdr, 0, sizeof(GtHdr), s);
+  if (zero_hdr) (void)hipMemsetAsync(w.hdr, 0, sizeof(GtHdr), s);
   if (w.win_bits == 16)
     k_gt_plan<16><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
                                                                   w.hdr, w.terms, w.chunk_req, w.chunk);

@@ -55,6 +55,10 @@ void launch_window_sums(const PointG2* reg, int nreg, PointG2* wsum, int nwin, h
 void launch_g1_combine(const PointG1* a, const PointG1* b, int n, uint8_t* out, hipStream_t s);
 void launch_checks_from_points(const PointG2* pks, const PointG1* sigs, int n, CheckIn* out, hipStream_t s);
 void launch_merge_codes(const int32_t* a, const int32_t* b, int n, int32_t* out, hipStream_t s);
+// level check + signature decode + verdict precedence of an aggregate batch in
+// one launch (pts, codes out); block 0 zeroes zero[0 .. zero_words) (<= 64)
+void launch_agg_prologue(const AggRequest* reqs, int n, uint32_t nreg, const uint8_t* sigs, int flavor, PointG1* pts,
+                         int32_t* codes, int* zero, int zero_words, hipStream_t s);
 void launch_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor, CheckIn* out, int32_t* codes,
                           hipStream_t s);
 void launch_pack_verdicts(const int32_t* codes, int n, uint8_t* bits, hipStream_t s);

@@ -90,6 +90,26 @@ __global__ __launch_bounds__(64) void k_decode_g1(const uint8_t* bytes, int n, i
   codes[i] = code;
 }
 
+// Everything an aggregate-verification batch needs before its fold, in one
+// launch (the GT path): the level check of processing.go:350-352, the
+// signature decode (SigBLS.UnmarshalBinary, a9) and the verdict precedence
+// sig decode error > level error > (fold: empty aggregate) > pairing verdict;
+// block 0 also zeroes `zero_words` words (the fold's range counters).
+__global__ __launch_bounds__(64) void k_agg_prologue(const AggRequest* reqs, int n, uint32_t nreg, const uint8_t* sigs,
+                                                     int flavor, PointG1* pts, int32_t* codes, int* zero,
+                                                     int zero_words) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && (int)threadIdx.x < zero_words) zero[threadIdx.x] = 0;
+  if (i >= n) return;
+  PointG1 P;
+  int32_t code = decode_g1_one(sigs + (size_t)i * 64, flavor, P);
+  pts[i] = P;
+  const AggRequest r = reqs[i];
+  const bool level_ok = r.bitlen == r.level_size && (uint64_t)r.offset + r.bitlen <= nreg;
+  if (code == HG_OK && !level_ok) code = HG_ERR_LEVEL;
+  codes[i] = code;
+}
+
 // The pairing-check inputs in one pass (hg_verify_batch*): 64 checks per
 // 128-thread block, wave 0 decodes the pks and wave 1 the sigs (the two run
 // side by side instead of one after the other), straight into CheckIn; pk
@@ -759,6 +779,10 @@ void launch_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int
 }
 void launch_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes, hipStream_t s) {
   if (n > 0) k_decode_g1<<<nblk(n, 64), 64, 0, s>>>(bytes, n, flavor, out, codes);
+}
+void launch_agg_prologue(const AggRequest* reqs, int n, uint32_t nreg, const uint8_t* sigs, int flavor, PointG1* pts,
+                         int32_t* codes, int* zero, int zero_words, hipStream_t s) {
+  if (n > 0) k_agg_prologue<<<nblk(n, 64), 64, 0, s>>>(reqs, n, nreg, sigs, flavor, pts, codes, zero, zero_words);
 }
 void launch_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor, CheckIn* out, int32_t* codes,
                           hipStream_t s) {

@@ -146,11 +146,17 @@ HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
   team_sync();
 }
 
-// Loads the G2Base line s (a, bx, cy: 6 Fp) into FA, FBX, FCY.
-HG_DEV void load_fixed_line(const Team& T, uint32_t* F, const LineCoef* tab, int s) {
-  const Fp* src = reinterpret_cast<const Fp*>(&tab[s]);
-  if (T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, src[T.tl]);
+// The G2Base line (a, bx, cy: 6 Fp) goes into FA, FBX, FCY from one VGPR
+// element per lane (lane tl < 6 holds Fp tl), read from the table one line
+// ahead so the L2 latency of the read overlaps the step's rounds.
+HG_DEV void fixed_line_fetch(const Team& T, Fp& held, const LineCoef* tab, int s) {
+  if (T.tl < 6 && s < kNumLines) held = reinterpret_cast<const Fp*>(&tab[s])[T.tl];
+}
+// publishes the held line, then fetches line `next`
+HG_DEV void load_fixed_line(const Team& T, uint32_t* F, Fp& held, const LineCoef* tab, int next) {
+  if (T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, held);
   team_sync();
+  fixed_line_fetch(T, held, tab, next);
 }
 
 // A point at infinity contributes the unit line (a = b = 0, c = 1). The
@@ -216,10 +222,13 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   constexpr XHint kLinePk = xh<ILinePk<S_F, S_F>>();
   t12_set_one(T, S_F);
   g2_regs_init(T, F, C);
+  Fp held;
+  fp_zero(held);
+  fixed_line_fetch(T, held, tab, 0);
   int s = 0;
   DIAG_T0();
   for (int i = kNafLen - 1; i > 0; i--) {
-    load_fixed_line(T, F, tab, s++);
+    load_fixed_line(T, F, held, tab, ++s);
     DIAG_ADD(0);
     if (i == kNafLen - 1) XInst<XP_PDBL_1>::run(T, S, xh<IMdbl2>());  // f = 1: no squaring
     else IMdbl1::run(T, S, xh<IMdbl2>());
@@ -233,16 +242,16 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
     x_line_pk<S_F, S_F>(T, S, d > 0 ? xh<AddPos::I1>() : d < 0 ? xh<AddNeg::I1>() : step);
     DIAG_ADD(3);
     if (d != 0) {
-      load_fixed_line(T, F, tab, s++);
+      load_fixed_line(T, F, held, tab, ++s);
       DIAG_ADD(0);
       if (d > 0) add_step<AddPos>(T, F, C, has_fixed, S, step);
       else add_step<AddNeg>(T, F, C, has_fixed, S, step);
       DIAG_ADD(4);
     }
   }
-  load_fixed_line(T, F, tab, s++);
+  load_fixed_line(T, F, held, tab, ++s);
   add_step<AddF1>(T, F, C, has_fixed, S, xh<AddF2::I1>());
-  load_fixed_line(T, F, tab, s++);
+  load_fixed_line(T, F, held, tab, ++s);
   add_step<AddF2>(T, F, C, has_fixed, S, after);
 }
 

@@ -69,8 +69,18 @@ HG_DEV void ld_f2(Fp2& r, const uint32_t* f12, int k) {
 // wait and the memory clobber keep the compiler from moving LDS accesses
 // across it) — and a workgroup barrier would be wrong in k_verify, whose two
 // waves run different programs between their shared barriers.
+//
+// No s_waitcnt: the LDS executes one wave's DS instructions in issue order,
+// so a read issued after a write (or a write after a read) of the same wave
+// sees it in that order without draining lgkmcnt; the compiler still waits
+// for each loaded register before its first use. At one wave per SIMD a
+// drain is a parked wave (SQ_WAIT_ANY), never hidden by another wave.
 HG_DEV void team_sync() {
+#ifdef HG_TEAM_SYNC_DRAIN
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+  asm volatile("" ::: "memory");
+#endif
   __builtin_amdgcn_wave_barrier();
 }
 

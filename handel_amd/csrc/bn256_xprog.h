@@ -130,6 +130,24 @@ HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t 
   for (int l = 0; l < 10; l++) out[l] = K >= 0 ? acc[l] : acc[l] + negk * kP2N[l];
 }
 
+// x_lincomb on operands already loaded (xs[t] = the element of term t)
+template <int W, int NT, int K>
+HG_DEV void x_lincomb_sum(const uint32_t (&w)[W], int base, const Fp (&xs)[NT], uint32_t (&out)[10]) {
+  uint32_t acc[10];
+#pragma unroll
+  for (int l = 0; l < 10; l++) acc[l] = K >= 0 ? (uint32_t)K * kP2N[l] : 0u;
+  uint32_t negk = 0;
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
+    const int32_t c = x_coef(w, base + t);
+    if constexpr (K < 0) negk += c < 0 ? (uint32_t)-c : 0u;
+#pragma unroll
+    for (int l = 0; l < 10; l++) acc[l] += (uint32_t)c * xs[t].l[l];
+  }
+#pragma unroll
+  for (int l = 0; l < 10; l++) out[l] = K >= 0 ? acc[l] : acc[l] + negk * kP2N[l];
+}
+
 // One job: sum of NP products of LDS operands plus NL R-shifted linear terms,
 // reduced once. Entries from `base`: NP x (u, v), NL x term, dst.
 //
@@ -273,12 +291,25 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   x_for<W>([&](auto i) { w[i] = S.w[i]; });
   if (nxt.off >= 0) x_fetch(T, S, nxt);
   if constexpr (NV > 0) {
+    // every lane evaluates every combination (a lane without one reads the
+    // ZERO register with coefficient 0: valid offsets, discarded result), and
+    // the values are pinned before the first store, so the compiler cannot
+    // sink a combination into its store's branch: the loads of all
+    // combinations issue together instead of one LDS latency per combination
+    Fp xs[NV][NT];
     x_for<NV>([&](auto v) {
-      constexpr int base = v * (1 + NT);
-      const uint32_t dst = x_off(w, base);
-      uint32_t val[10];
-      x_lincomb<W, NT, KP>(T, w, base + 1, val);
-      if (dst != 0xffffu) st_fp_a8(x_at(T, dst), val);
+      x_for<NT>([&](auto t) { ld_fp_a8(xs[v][t], x_at(T, x_term_off(w, v * (1 + NT) + 1 + t))); });
+    });
+    __builtin_amdgcn_sched_barrier(0);  // every load of the pre-pass in flight before the first sum
+    uint32_t val[NV][10];
+    x_for<NV>([&](auto v) { x_lincomb_sum<W, NT, KP>(w, v * (1 + NT) + 1, xs[v], val[v]); });
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+#pragma unroll
+      for (int l = 0; l < 10; l++) asm volatile("" : "+v"(val[v][l]));
+    x_for<NV>([&](auto v) {
+      const uint32_t dst = x_off(w, v * (1 + NT));
+      if (dst != 0xffffu) st_fp_a8(x_at(T, dst), val[v]);
     });
     team_sync();
   }

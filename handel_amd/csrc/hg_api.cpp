@@ -497,8 +497,17 @@ static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
   return HG_OK;
 }
 
+// the level check of processing.go:350-352 on the device
+__global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool ok = r[i].bitlen == r[i].level_size && (uint64_t)r[i].offset + r[i].bitlen <= nreg;
+  out[i] = ok ? HG_OK : HG_ERR_LEVEL;
+}
+
 // The Combine fold and (verify) the pairing check of n requests, device
-// pointers, on stream s; d_lvl holds the level codes and is updated in place.
+// pointers, on stream s; d_lvl holds the level codes and is updated in place
+// (nullptr: computed here when the flow needs them).
 static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
                                    const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
                                    bool verify, hipStream_t s) {
@@ -522,6 +531,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
   }
   if (d_agg) HG_CHECK(c, c->pts2.ensure(n));
+  if (!d_lvl) HG_CHECK(c, c->codes_c.ensure(n));
   if (verify) {
     HG_CHECK(c, c->pts1.ensure(n));
     HG_CHECK(c, c->codes_b.ensure(n));
@@ -533,13 +543,35 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   }
   gw.win_bits = level == 2 ? 16 : 8;
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
+  if (use_gt && !g2_fold) {
+    // GT path, verdicts only: level check, signature decode and the fold's
+    // counters in one launch, then the fold and the check on d_codes
+    launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, c->pts1.p, d_codes, (int*)gw.hdr,
+                        (int)(sizeof(GtHdr) / sizeof(int)), s);
+    PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
+    launch_gt_fold(d_reqs, (int)n, d_words, d_codes, (int)c->nreg, c->block_levels,
+                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, false, s);
+    fold.stop();
+    PhaseTimer t(c, HG_PHASE_VERIFY, s);
+    launch_verify_sig(c->pts1.p, (int)n, c->d_lines, c->gt_y.p, d_codes, s);
+    t.stop();
+    all.stop();
+    int rc = check_launch(c);
+    if (rc) return rc;
+    HG_CHECK(c, end(c, s));
+    return HG_OK;
+  }
+  if (!d_lvl) {
+    d_lvl = c->codes_c.p;
+    k_level_codes<<<nb(n), 256, 0, s>>>(d_reqs, (int)n, (uint32_t)c->nreg, d_lvl);
+  }
   PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
   if (g2_fold)
     launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
                      d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
   if (use_gt)
     launch_gt_fold(d_reqs, (int)n, d_words, d_lvl, (int)c->nreg, c->block_levels,
-                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, s);
+                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, true, s);
   fold.stop();
   if (d_agg) {
     launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);
@@ -562,13 +594,6 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   if (rc) return rc;
   HG_CHECK(c, end(c, s));
   return HG_OK;
-}
-
-__global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t* out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  bool ok = r[i].bitlen == r[i].level_size && (uint64_t)r[i].offset + r[i].bitlen <= nreg;
-  out[i] = ok ? HG_OK : HG_ERR_LEVEL;
 }
 
 static int aggregate_host_locked(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
@@ -868,10 +893,7 @@ int hg_verify_aggregate_device(hg_ctx* c, const hg_request* d_reqs, size_t n, co
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  HG_CHECK(c, c->codes_c.ensure(n));
-  HG_CHECK(c, begin(c, s));
-  k_level_codes<<<nb(n), 256, 0, s>>>(d_reqs, (int)n, (uint32_t)c->nreg, c->codes_c.p);
-  return aggregate_device_locked(c, d_reqs, n, d_words, d_sigs, d_codes, d_agg_pk_out, c->codes_c.p, true, s);
+  return aggregate_device_locked(c, d_reqs, n, d_words, d_sigs, d_codes, d_agg_pk_out, nullptr, true, s);
 }
 
 int hg_verify_aggregate(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,
