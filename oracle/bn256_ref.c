@@ -1193,6 +1193,23 @@ static int verify_points(const g1p* hm, int pk_inf, const fp2* qx, const fp2* qy
   return f12_is_one(&e1) ? RC_OK : RC_SIG_INVALID;
 }
 
+/* ref_set_rehash(1): every check hashes the message itself, as the reference's
+ * PublicKey.VerifySignature does on every call (bn256/go/bn256.go:82-94 calls
+ * hashedMessage, :210-218: SHA-256, the rand.Int rule and a G1 scalar
+ * multiplication); 0 (default): once per batch. Set before a batch starts. */
+static int g_rehash = 0;
+static const uint8_t* g_msg = 0;
+static size_t g_msglen = 0;
+void ref_set_rehash(int on) { g_rehash = on; }
+/* the hashed message of one check: the batch's, or recomputed (g_rehash) */
+static const g1p* check_hm(const g1p* batch_hm, g1p* own) {
+  if (!g_rehash) return batch_hm;
+  uint8_t k[32];
+  if (ref_hash_scalar(g_msg, g_msglen, k) != RC_OK) return batch_hm;
+  hash_point(own, k);
+  return own;
+}
+
 typedef struct {
   const uint8_t* pks;
   const uint8_t* sigs;
@@ -1212,7 +1229,8 @@ static void* verify_worker(void* arg) {
     if (rc) { j->codes[i] = RC_PK_UNMARSHAL; continue; }
     rc = dec_g1(j->sigs + 64 * i, 64, j->flavor, &sx, &sy, &sinf);
     if (rc) { j->codes[i] = RC_SIG_UNMARSHAL; continue; }
-    j->codes[i] = verify_points(j->hm, pinf, &qx, &qy, sinf, &sx, &sy, j->fast);
+    g1p own;
+    j->codes[i] = verify_points(check_hm(j->hm, &own), pinf, &qx, &qy, sinf, &sx, &sy, j->fast);
   }
   return 0;
 }
@@ -1228,6 +1246,8 @@ long ref_verify_batch(const uint8_t* msg, size_t msglen, const uint8_t* pks, con
   }
   g1p hm;
   hash_point(&hm, k);
+  g_msg = msg;
+  g_msglen = msglen;
   if (nthreads < 1) nthreads = 1;
   if ((size_t)nthreads > n && n > 0) nthreads = (int)n;
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
@@ -1292,7 +1312,8 @@ static void* agg_worker(void* arg) {
     fp2 qx = F2_ZERO, qy = F2_ZERO;
     int pinf = g2_is_inf(&acc);
     if (!pinf) g2_affine(&qx, &qy, &acc);
-    j->codes[r] = verify_points(j->hm, pinf, &qx, &qy, sinf, &sx, &sy, j->fast);
+    g1p own;
+    j->codes[r] = verify_points(check_hm(j->hm, &own), pinf, &qx, &qy, sinf, &sx, &sy, j->fast);
   }
   return 0;
 }
@@ -1307,6 +1328,8 @@ long ref_verify_aggregate(const uint8_t* msg, size_t msglen, const uint8_t* reg,
   int hash_ok = ref_hash_scalar(msg, msglen, k) == RC_OK;
   g1p hm;
   if (hash_ok) hash_point(&hm, k);
+  g_msg = msg;
+  g_msglen = msglen;
   if (nthreads < 1) nthreads = 1;
   if ((size_t)nthreads > nreq && nreq > 0) nthreads = (int)nreq;
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);

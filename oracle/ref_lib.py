@@ -35,6 +35,8 @@ def lib():
         u8p = ctypes.c_void_p
         L.ref_init.restype = None
         L.ref_pair.argtypes = [u8p, u8p, u8p]
+        L.ref_set_rehash.restype = None
+        L.ref_set_rehash.argtypes = [ctypes.c_int]
         L.ref_verify_batch.restype = ctypes.c_long
         L.ref_verify_batch.argtypes = [u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_size_t, u8p,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -64,6 +66,11 @@ def pair(g1: bytes, g2: bytes) -> bytes:
     if rc:
         raise ValueError(f"decode error {rc}")
     return out.raw
+
+
+def set_rehash(on: bool) -> None:
+    """Hash the message per check (the reference's VerifySignature does) instead of once per batch."""
+    lib().ref_set_rehash(1 if on else 0)
 
 
 def verify_batch(msg: bytes, pks: bytes, sigs: bytes, nthreads: int = 1, flavor: int = 0,

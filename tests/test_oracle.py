@@ -157,6 +157,21 @@ def test_product_form_matches_reference_verdicts():
     assert list(a) == py
 
 
+def test_rehash_per_check_matches_batch_hash():
+    """bench.py's CPU baseline hashes the message on every check, as the
+    reference's VerifySignature does (bn256/go/bn256.go:82-94): same verdicts."""
+    msg = F.TEST_MESSAGES[0]
+    ks, pks, sigs = F.keys_and_sigs(4, msg=msg, seed=b"rehash")
+    sigs = F.tamper(sigs, every=2)
+    once = R.verify_batch(msg, pks, sigs, nthreads=2, fast=2)
+    R.set_rehash(True)
+    try:
+        each = R.verify_batch(msg, pks, sigs, nthreads=2, fast=2)
+    finally:
+        R.set_rehash(False)
+    assert list(once) == list(each) == [1, 0, 1, 0]
+
+
 def test_algorithmic_work_per_check_is_pinned():
     """bench.py's roofline work figure = the oracle's op counter for one check
     of the algorithm the GPU runs (fast=2)."""
