@@ -174,12 +174,10 @@ HG_DEV void acc_mad_pinned(Acc& a, const Fp& x, const Fp& y) {
       asm("" : "+v"(a.c[i + j]));
     }
 }
+// a, b: the first product's operands, already loaded by the caller
 template <int W, int NP>
-HG_DEV void x_products(const Team& T, const uint32_t (&w)[W], int base, Acc& acc) {
+HG_DEV void x_products(const Team& T, const uint32_t (&w)[W], int base, Acc& acc, Fp a, Fp b) {
   if constexpr (NP > 0) {
-    Fp a, b;
-    ld_fp_a8(a, x_at(T, x_off(w, base)));
-    ld_fp_a8(b, x_at(T, x_off(w, base + 1)));
     x_for<NP>([&](auto p) {
       Fp a2, b2;
       if constexpr (p + 1 < NP) {
@@ -231,13 +229,10 @@ HG_DEV void kacc_mad_pinned(KAcc& k, const Fp& x, const Fp& y) {
     }
 }
 template <int W, int NP>
-HG_DEV void x_products_ks(const Team& T, const uint32_t (&w)[W], int base, Acc& acc) {
+HG_DEV void x_products_ks(const Team& T, const uint32_t (&w)[W], int base, Acc& acc, Fp a, Fp b) {
   KAcc k;
 #pragma unroll
   for (int c = 0; c < 9; c++) k.z0[c] = k.z1[c] = k.z2[c] = 0;
-  Fp a, b;
-  ld_fp_a8(a, x_at(T, x_off(w, base)));
-  ld_fp_a8(b, x_at(T, x_off(w, base + 1)));
   x_for<NP>([&](auto p) {
     Fp a2, b2;
     if constexpr (p + 1 < NP) {
@@ -266,14 +261,23 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
   Acc acc;
   acc_zero(acc);
   constexpr int lbase = 2 * NP;
+  // the linear terms' elements and the first product's operands are loaded
+  // together, so the job pays one LDS round trip before its first mad
+  Fp lx[NL > 0 ? NL : 1];
+  if constexpr (NL > 0) x_for<NL>([&](auto t) { ld_fp_a8(lx[t], x_at(T, x_term_off(w, base + lbase + t))); });
+  Fp a0, b0;
+  if constexpr (NP > 0) {
+    ld_fp_a8(a0, x_at(T, x_off(w, base)));
+    ld_fp_a8(b0, x_at(T, x_off(w, base + 1)));
+  }
   if constexpr (NL > 0) {
     uint32_t val[10];
-    x_lincomb<W, NL, KL>(T, w, base + lbase, val);
+    x_lincomb_sum<W, NL, KL>(w, base + lbase, lx, val);
 #pragma unroll
     for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] = val[l];
   }
-  if constexpr (KS) x_products_ks<W, NP>(T, w, base, acc);
-  else x_products<W, NP>(T, w, base, acc);
+  if constexpr (KS) x_products_ks<W, NP>(T, w, base, acc, a0, b0);
+  else x_products<W, NP>(T, w, base, acc, a0, b0);
   dst = x_off(w, base + lbase + NL);
   if constexpr (NL > 0) acc_reduce_wide(r, acc);  // linear terms: result < 31p
   else acc_reduce(r, acc);                        // products only: < 2p, one subtraction

@@ -275,3 +275,63 @@ def test_registry_above_16key_limit_uses_8key_tables(engine):
     codes = engine.verify_aggregate(reqs, words, sigs)
     assert list(codes) == list(_oracle(F.LIB_MESSAGE, reg, reqs, words, sigs))
     assert list(codes) == [1, 0, 1, 0]
+
+
+def test_error_precedence_on_gt_path(engine):
+    """Verdict precedence of the GT path's prologue kernel (k_agg_prologue +
+    k_gt_plan), through the host and the device entry points: signature decode
+    error (the packet parse, before processing) > level error
+    (processing.go:350-352) > empty bitset (the nil-aggregate panic) > pairing
+    verdict. Single-error rows are also checked against the oracle."""
+    import torch
+
+    n = 32
+    ks = F.scalars(n, seed=b"gt-prec")
+    reg = R.g2_scalar_base(F.scalar_bytes(ks))
+    assert list(engine.registry_load(reg)) == [0] * n
+    msg = F.LIB_MESSAGE
+    assert engine.set_message(msg) == 0
+    assert engine.prepare_aggregate() == 0
+    h = O.hashed_message(msg)[0]
+    off_curve = (1).to_bytes(32, "big") + (1).to_bytes(32, "big")
+
+    def honest(off, bits):
+        k = sum(ks[off + i] for i, b in enumerate(bits) if b and off + i < n) % O.ORDER
+        return O.g1_marshal(O.g1_mul(h, k))
+
+    rows = [  # (offset, level size, bits, signature, expected code)
+        (0, 8, [True, True] + [False] * 6, None, 0),
+        (8, 16, [True] * 8, off_curve, 5),        # bad signature beats the level error
+        (8, 16, [False] * 8, None, 3),            # level error beats the empty bitset
+        (16, 8, [False] * 8, None, 6),            # empty bitset: nil aggregate
+        (16, 8, [False] * 8, off_curve, 5),       # bad signature beats the empty bitset
+        (24, 16, [True] * 16, None, 3),           # range past the registry
+        (0, 16, [True] * 16, "tamper", 1),        # pairing verdict
+    ]
+    ranges, bitsets, sigs = [], [], bytearray()
+    for off, size, bits, sig, _ in rows:
+        ranges.append((off, size))
+        bitsets.append(bits)
+        if sig is None:
+            sigs += honest(off, bits) if any(bits) else honest(0, [True])
+        elif sig == "tamper":
+            s = honest(off, bits)
+            sigs += O.g1_marshal(O.g1_add(O.g1_unmarshal(s)[0], O.g1_unmarshal(honest(0, [True]))[0]))
+        else:
+            sigs += sig
+    reqs, words = F.pack_requests(ranges, bitsets)
+    reqs = np.array(reqs, dtype=REQ_DTYPE)
+    want = [code for *_, code in rows]
+    assert list(engine.verify_aggregate(reqs, words, bytes(sigs))) == want
+    single = [0, 2, 3, 5, 6]  # rows with at most one error: the oracle agrees
+    oracle = _oracle(msg, reg, reqs, words, bytes(sigs))
+    assert [int(oracle[i]) for i in single] == [want[i] for i in single]
+    dev = torch.device("cuda", 0)
+    d_reqs = torch.frombuffer(bytearray(reqs.tobytes()), dtype=torch.uint8).to(dev)
+    d_words = torch.frombuffer(bytearray(words.tobytes()), dtype=torch.uint8).to(dev)
+    d_sigs = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
+    d_codes = torch.full((len(rows),), -1, dtype=torch.int32, device=dev)
+    engine.verify_aggregate_device(d_reqs.data_ptr(), len(rows), d_words.data_ptr(), d_sigs.data_ptr(),
+                                   d_codes.data_ptr(), 0, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert d_codes.cpu().tolist() == want
