@@ -335,3 +335,36 @@ def test_error_precedence_on_gt_path(engine):
                                    d_codes.data_ptr(), 0, torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
     assert d_codes.cpu().tolist() == want
+
+
+@pytest.mark.parametrize("seed,n_reg,m", [(1, 37, 1), (2, 100, 7), (3, 257, 64), (4, 1000, 300), (5, 1000, 777),
+                                          (6, 4000, 129)])
+def test_random_batches_match_oracle(engine, seed, n_reg, m):
+    """Randomised GT-path batches against the oracle: random registry sizes,
+    random nodes and Handel levels (partitioner rangeLevel), bitset densities
+    from empty to full (so plain, complemented and empty folds all occur),
+    every 5th aggregate tampered."""
+    rng = np.random.default_rng(seed)
+    ks = F.scalars(n_reg, seed=b"gt-rand-%d" % seed)
+    reg = engine.keygen(F.scalar_bytes(ks))
+    assert not engine.registry_load(reg).any()
+    msg = F.LIB_MESSAGE
+    assert engine.set_message(msg) == 0
+    assert engine.prepare_aggregate() == 0
+    levels = _levels(n_reg, [int(x) for x in rng.integers(0, n_reg, size=8)])
+    ranges = [levels[int(i)] for i in rng.integers(0, len(levels), size=m)]
+    bitsets = []
+    for _, size in ranges:
+        d = float(rng.choice([0.0, 0.02, rng.uniform(0.5, 1.0), 0.97, 1.0]))
+        bitsets.append([bool(b) for b in rng.random(size) < d])
+    scal = bytearray()
+    for (off, _), bits in zip(ranges, bitsets):
+        k = sum(ks[off + i] for i, b in enumerate(bits) if b) % O.ORDER
+        scal += (k if k else 1).to_bytes(32, "big")
+    sigs = F.tamper(engine.sign(bytes(scal)), every=5)
+    reqs, words = F.pack_requests(ranges, bitsets)
+    reqs = np.array(reqs, dtype=REQ_DTYPE)
+    got = engine.verify_aggregate(reqs, words, sigs)
+    want = _oracle(msg, reg, reqs, words, sigs)
+    assert list(got) == list(want)
+    assert (got == 0).any() or m < 8
