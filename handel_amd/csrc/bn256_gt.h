@@ -23,8 +23,9 @@ struct GtReq {
   int term_off;   // first term in the batch's term list
   int chunk_off;  // first chunk in the batch's chunk list
 };
-struct GtHdr {
-  int terms, chunks;
+struct alignas(8) GtHdr {
+  int terms, chunks;  // one 64-bit atomic in k_gt_plan
+  int big, mid;       // requests k_gt_combine finishes: > 4 chunks / 2..4 chunks (one 64-bit atomic)
 };
 // level k >= 4 block j of the registry at blk[base[k] + j] (levels <= 3 are
 // entries of the window table in use)
@@ -38,6 +39,7 @@ struct GtWork {
   uint32_t* terms;
   int* chunk_req;
   Gt* partial;
+  int* multi;      // 2n: the big requests from 0, the mid ones from n (k_gt_combine's order)
   int chunk_grid;  // workgroups of k_gt_chunks (4 teams each)
   int chunk;       // terms per chunk
   int win_bits;    // 8 or 16: which window table `win` is

@@ -286,9 +286,9 @@ template <int W>
 __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* reqs, int n, const uint64_t* words,
                                                              int32_t* codes, int nreg, int levels, GtBlockIndex bi,
                                                              GtReq* plan, GtHdr* hdr, uint32_t* terms,
-                                                             int* chunk_req, int chunk) {
+                                                             int* chunk_req, int chunk, int* multi) {
   constexpr uint32_t kUnits = 64 / W, kMask = (1u << W) - 1u, kShift = W == 8 ? 3 : 4;
-  __shared__ int sm[kPlanWaves], sc[kPlanWaves], base_m, base_c;
+  __shared__ int sm[kPlanWaves], sc[kPlanWaves], sb[kPlanWaves], sd[kPlanWaves], base_m, base_c, base_b, base_d;
   const int wv = threadIdx.x >> 6;
   const int r = blockIdx.x * kPlanWaves + wv;
   const int lane = threadIdx.x & 63;
@@ -322,28 +322,51 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
       g.chunks = (g.m + chunk - 1) / chunk;
     }
   }
-  // ranges in the batch's term and chunk lists: one atomic per workgroup
+  // ranges in the batch's term and chunk lists, and places in k_gt_combine's
+  // request lists (requests of more than 4 chunks first, so the combine's
+  // longest requests start first, on SIMDs of their own): one atomic per
+  // workgroup and list
+  const bool big = g.chunks > 4, mid = g.chunks >= 2 && g.chunks <= 4;
   if (lane == 0) {
     sm[wv] = g.m;
     sc[wv] = g.chunks;
+    sb[wv] = big ? 1 : 0;
+    sd[wv] = mid ? 1 : 0;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int tm = 0, tc = 0;
+    int tm = 0, tc = 0, tb = 0, td = 0;
     for (int i = 0; i < kPlanWaves; i++) {
-      const int m = sm[i], c = sc[i];
+      const int m = sm[i], c = sc[i], b = sb[i], d = sd[i];
       sm[i] = tm;
       sc[i] = tc;
+      sb[i] = tb;
+      sd[i] = td;
       tm += m;
       tc += c;
+      tb += b;
+      td += d;
     }
-    base_m = tm ? atomicAdd(&hdr->terms, tm) : 0;
-    base_c = tc ? atomicAdd(&hdr->chunks, tc) : 0;
+    // two 64-bit atomics: (terms, chunks) and (big, mid) are adjacent int
+    // pairs (little-endian halves; neither low half can carry into the high one)
+    unsigned long long tc2 = 0, bd2 = 0;
+    if (tm | tc)
+      tc2 = atomicAdd(reinterpret_cast<unsigned long long*>(&hdr->terms),
+                      (unsigned long long)(unsigned)tm | ((unsigned long long)(unsigned)tc << 32));
+    if (tb | td)
+      bd2 = atomicAdd(reinterpret_cast<unsigned long long*>(&hdr->big),
+                      (unsigned long long)(unsigned)tb | ((unsigned long long)(unsigned)td << 32));
+    base_m = (int)(unsigned)tc2;
+    base_c = (int)(tc2 >> 32);
+    base_b = (int)(unsigned)bd2;
+    base_d = (int)(bd2 >> 32);
   }
   __syncthreads();
   g.term_off = base_m + sm[wv];
   g.chunk_off = base_c + sc[wv];
   if (r < n && lane == 0) plan[r] = g;
+  if (lane == 0 && big) multi[base_b + sb[wv]] = r;
+  if (lane == 0 && mid) multi[n + base_d + sd[wv]] = r;
   if (!go) return;  // no barrier below
   uint32_t at = g.term_off;
   if (g.comp) {
@@ -454,13 +477,15 @@ __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, 
 
 // Combine (one wave per request of two or more chunks): the 4 teams multiply
 // every 4th partial, a 2-level tree joins them into Y.
-__global__ __launch_bounds__(64) void k_gt_combine(int n, const int32_t* codes, const GtReq* plan,
+// Workgroup b takes the b-th request of the big list, then of the mid list
+// (k_gt_plan), so the requests with the longest chains are dispatched first.
+__global__ __launch_bounds__(64) void k_gt_combine(int n, const GtHdr* hdr, const int* multi, const GtReq* plan,
                                                    const Gt* partial, Gt* y) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
-  const int r = blockIdx.x;
-  if (r >= n || codes[r] != HG_OK) return;  // one request per wave: uniform
+  const int b = blockIdx.x, nbig = hdr->big;
+  if (b >= nbig + hdr->mid) return;  // one request per wave: uniform
+  const int r = b < nbig ? multi[b] : multi[n + b - nbig];
   const GtReq g = plan[r];
-  if (g.chunks < 2) return;
   Team T = make_team(lds, kFoldWords);
   fold_regs_init(T);
   const int team = (threadIdx.x & 63) >> 4;
@@ -633,12 +658,12 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
   if (zero_hdr) (void)hipMemsetAsync(w.hdr, 0, sizeof(GtHdr), s);
   if (w.win_bits == 16)
     k_gt_plan<16><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
-                                                                  w.hdr, w.terms, w.chunk_req, w.chunk);
+                                                                  w.hdr, w.terms, w.chunk_req, w.chunk, w.multi);
   else
     k_gt_plan<8><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
-                                                                 w.hdr, w.terms, w.chunk_req, w.chunk);
+                                                                 w.hdr, w.terms, w.chunk_req, w.chunk, w.multi);
   k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.chunk_req, w.plan, w.hdr, w.chunk, w.partial, y);
-  k_gt_combine<<<n, 64, 0, s>>>(n, codes, w.plan, w.partial, y);
+  k_gt_combine<<<n, 64, 0, s>>>(n, w.hdr, w.multi, w.plan, w.partial, y);
 }
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
   if (n > 0) k_verify_sig<4><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, y, codes);
