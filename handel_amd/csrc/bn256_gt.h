@@ -26,6 +26,7 @@ struct GtReq {
 struct alignas(8) GtHdr {
   int terms, chunks;  // one 64-bit atomic in k_gt_plan
   int big, mid;       // requests k_gt_combine finishes: > 4 chunks / 2..4 chunks (one 64-bit atomic)
+  int nlong, nshort;  // chunks of more / at most half the chunk size in k_gt_chunks' order (one 64-bit atomic)
 };
 // level k >= 4 block j of the registry at blk[base[k] + j] (levels <= 3 are
 // entries of the window table in use)
@@ -37,7 +38,8 @@ struct GtWork {
   GtReq* plan;
   GtHdr* hdr;
   uint32_t* terms;
-  int* chunk_req;
+  int2* ord;       // k_gt_chunks' order: (chunk, request), long chunks from 0, short ones down from cap - 1
+  int cap;         // entries of ord and partial
   Gt* partial;
   int* multi;      // 2n: the big requests from 0, the mid ones from n (k_gt_combine's order)
   int chunk_grid;  // workgroups of k_gt_chunks (4 teams each)

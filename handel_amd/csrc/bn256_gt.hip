@@ -286,9 +286,10 @@ template <int W>
 __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* reqs, int n, const uint64_t* words,
                                                              int32_t* codes, int nreg, int levels, GtBlockIndex bi,
                                                              GtReq* plan, GtHdr* hdr, uint32_t* terms,
-                                                             int* chunk_req, int chunk, int* multi) {
+                                                             int2* ord, int cap, int chunk, int* multi) {
   constexpr uint32_t kUnits = 64 / W, kMask = (1u << W) - 1u, kShift = W == 8 ? 3 : 4;
-  __shared__ int sm[kPlanWaves], sc[kPlanWaves], sb[kPlanWaves], sd[kPlanWaves], base_m, base_c, base_b, base_d;
+  __shared__ int sm[kPlanWaves], sc[kPlanWaves], sb[kPlanWaves], sd[kPlanWaves], sl[kPlanWaves], ss[kPlanWaves];
+  __shared__ int base_m, base_c, base_b, base_d, base_l, base_s;
   const int wv = threadIdx.x >> 6;
   const int r = blockIdx.x * kPlanWaves + wv;
   const int lane = threadIdx.x & 63;
@@ -327,39 +328,61 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
   // longest requests start first, on SIMDs of their own): one atomic per
   // workgroup and list
   const bool big = g.chunks > 4, mid = g.chunks >= 2 && g.chunks <= 4;
+  // k_gt_chunks' order: every chunk longer than half the chunk size first
+  // (a request's full chunks and a long tail), the short tails last, so the
+  // waves of the first resident round carry the long product chains
+  const int tail = g.m % chunk;
+  const int nshort = (tail > 0 && 2 * tail <= chunk) ? 1 : 0, nlong = g.chunks - nshort;
   if (lane == 0) {
     sm[wv] = g.m;
     sc[wv] = g.chunks;
     sb[wv] = big ? 1 : 0;
     sd[wv] = mid ? 1 : 0;
+    sl[wv] = nlong;
+    ss[wv] = nshort;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int tm = 0, tc = 0, tb = 0, td = 0;
-    for (int i = 0; i < kPlanWaves; i++) {
-      const int m = sm[i], c = sc[i], b = sb[i], d = sd[i];
-      sm[i] = tm;
-      sc[i] = tc;
-      sb[i] = tb;
-      sd[i] = td;
-      tm += m;
-      tc += c;
-      tb += b;
-      td += d;
+  if (threadIdx.x < 64) {  // wave 0: lanes i < kPlanWaves scan wave i's counts side by side
+    const int i = threadIdx.x;
+    const bool in = i < kPlanWaves;
+    int v[6] = {in ? sm[i] : 0, in ? sc[i] : 0, in ? sb[i] : 0, in ? sd[i] : 0, in ? sl[i] : 0, in ? ss[i] : 0};
+    int inc[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) inc[j] = v[j];
+#pragma unroll
+    for (int d = 1; d < kPlanWaves; d <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        const int x = __shfl_up(inc[j], d);
+        if (i >= d) inc[j] += x;
+      }
     }
-    // two 64-bit atomics: (terms, chunks) and (big, mid) are adjacent int
-    // pairs (little-endian halves; neither low half can carry into the high one)
-    unsigned long long tc2 = 0, bd2 = 0;
-    if (tm | tc)
-      tc2 = atomicAdd(reinterpret_cast<unsigned long long*>(&hdr->terms),
-                      (unsigned long long)(unsigned)tm | ((unsigned long long)(unsigned)tc << 32));
-    if (tb | td)
-      bd2 = atomicAdd(reinterpret_cast<unsigned long long*>(&hdr->big),
-                      (unsigned long long)(unsigned)tb | ((unsigned long long)(unsigned)td << 32));
-    base_m = (int)(unsigned)tc2;
-    base_c = (int)(tc2 >> 32);
-    base_b = (int)(unsigned)bd2;
-    base_d = (int)(bd2 >> 32);
+    int tot[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) tot[j] = __shfl(inc[j], kPlanWaves - 1);
+    if (in) {
+      sm[i] = inc[0] - v[0];
+      sc[i] = inc[1] - v[1];
+      sb[i] = inc[2] - v[2];
+      sd[i] = inc[3] - v[3];
+      sl[i] = inc[4] - v[4];
+      ss[i] = inc[5] - v[5];
+    }
+    if (i == 0) {
+      // three 64-bit atomics, issued together (no branch between them): the
+      // counter pairs (terms, chunks), (big, mid), (nlong, nshort) are adjacent
+      // ints (little-endian halves; no low half can carry into its high one)
+      typedef unsigned long long u64;
+      const u64 tc2 = atomicAdd(reinterpret_cast<u64*>(&hdr->terms), (u64)(unsigned)tot[0] | ((u64)(unsigned)tot[1] << 32));
+      const u64 bd2 = atomicAdd(reinterpret_cast<u64*>(&hdr->big), (u64)(unsigned)tot[2] | ((u64)(unsigned)tot[3] << 32));
+      const u64 ls2 = atomicAdd(reinterpret_cast<u64*>(&hdr->nlong), (u64)(unsigned)tot[4] | ((u64)(unsigned)tot[5] << 32));
+      base_m = (int)(unsigned)tc2;
+      base_c = (int)(tc2 >> 32);
+      base_b = (int)(unsigned)bd2;
+      base_d = (int)(bd2 >> 32);
+      base_l = (int)(unsigned)ls2;
+      base_s = (int)(ls2 >> 32);
+    }
   }
   __syncthreads();
   g.term_off = base_m + sm[wv];
@@ -403,7 +426,9 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
     }
     at += __shfl(inc, 63);
   }
-  for (int c = lane; c < g.chunks; c += 64) chunk_req[g.chunk_off + c] = r;
+  const int lo = base_l + sl[wv];
+  for (int c = lane; c < nlong; c += 64) ord[lo + c] = make_int2(g.chunk_off + c, r);
+  if (nshort && lane == 0) ord[cap - 1 - (base_s + ss[wv])] = make_int2(g.chunk_off + g.chunks - 1, r);
 }
 
 // Chunks: each team multiplies the (at most `chunk`) terms of one chunk. A
@@ -413,21 +438,23 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
 // The next term is fetched from HBM into registers while the current product
 // runs.
 __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, const uint32_t* terms,
-                                                  const int* chunk_req, const GtReq* plan, const GtHdr* hdr,
+                                                  const int2* ord, int cap, const GtReq* plan, const GtHdr* hdr,
                                                   int chunk, Gt* partial, Gt* y) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
   Team T = make_team(lds, kFoldWords);
   fold_regs_init(T);
   const int team = (threadIdx.x & 63) >> 4;
-  const int total = hdr->chunks;
+  const int total = hdr->chunks, nlong = hdr->nlong;
   XStream S = x_stream();
   for (int base = blockIdx.x * 4; base < total; base += gridDim.x * 4) {  // wave-uniform
-    const int c = base + team;
-    const bool valid = c < total;
-    int first = 0, cnt = 0, r = 0;
+    const int k = base + team;
+    const bool valid = k < total;
+    int first = 0, cnt = 0, r = 0, c = 0;
     bool single = false;
     if (valid) {
-      r = chunk_req[c];
+      const int2 e = k < nlong ? ord[k] : ord[cap - 1 - (k - nlong)];
+      c = e.x;
+      r = e.y;
       const GtReq g = plan[r];
       first = g.term_off + (c - g.chunk_off) * chunk;
       cnt = min(chunk, g.term_off + g.m - first);
@@ -658,11 +685,11 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
   if (zero_hdr) (void)hipMemsetAsync(w.hdr, 0, sizeof(GtHdr), s);
   if (w.win_bits == 16)
     k_gt_plan<16><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
-                                                                  w.hdr, w.terms, w.chunk_req, w.chunk, w.multi);
+                                                                  w.hdr, w.terms, w.ord, w.cap, w.chunk, w.multi);
   else
     k_gt_plan<8><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
-                                                                 w.hdr, w.terms, w.chunk_req, w.chunk, w.multi);
-  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.chunk_req, w.plan, w.hdr, w.chunk, w.partial, y);
+                                                                 w.hdr, w.terms, w.ord, w.cap, w.chunk, w.multi);
+  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.ord, w.cap, w.plan, w.hdr, w.chunk, w.partial, y);
   k_gt_combine<<<n, 64, 0, s>>>(n, w.hdr, w.multi, w.plan, w.partial, y);
 }
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {

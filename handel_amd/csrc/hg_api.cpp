@@ -189,7 +189,8 @@ struct hg_ctx {
   DevBuf<GtReq> gt_plan;
   DevBuf<GtHdr> gt_hdr;
   DevBuf<uint32_t> gt_terms;
-  DevBuf<int> gt_chunk_req, gt_multi;
+  DevBuf<int2> gt_ord;
+  DevBuf<int> gt_multi;
   DevBuf<Gt> gt_partial, gt_y;
   // submission order across streams: the event recorded after the last
   // submission and the stream it ran on (the workspaces above are shared)
@@ -295,7 +296,7 @@ static void release_all(hg_ctx* c) {
   c->gt_plan.release();
   c->gt_hdr.release();
   c->gt_terms.release();
-  c->gt_chunk_req.release();
+  c->gt_ord.release();
   c->gt_multi.release();
   c->gt_partial.release();
   c->gt_y.release();
@@ -485,14 +486,15 @@ static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
   HG_CHECK(c, c->gt_plan.ensure(n));
   HG_CHECK(c, c->gt_hdr.ensure(1));
   HG_CHECK(c, c->gt_terms.ensure(n * mmax));
-  HG_CHECK(c, c->gt_chunk_req.ensure(n * cmax));
+  HG_CHECK(c, c->gt_ord.ensure(n * cmax));
   HG_CHECK(c, c->gt_multi.ensure(2 * n));
   HG_CHECK(c, c->gt_partial.ensure(n * cmax));
   HG_CHECK(c, c->gt_y.ensure(n));
   w.plan = c->gt_plan.p;
   w.hdr = c->gt_hdr.p;
   w.terms = c->gt_terms.p;
-  w.chunk_req = c->gt_chunk_req.p;
+  w.ord = c->gt_ord.p;
+  w.cap = (int)(n * cmax);
   w.multi = c->gt_multi.p;
   w.partial = c->gt_partial.p;
   w.chunk_grid = grid;
