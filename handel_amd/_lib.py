@@ -55,6 +55,10 @@ SIGNATURES = {
     "hg_registry_size": (_SZ, [_P]),
     "hg_prepare_aggregate": (_I, [_P]),
     "hg_aggregate_tables": (_I, [_P]),
+    "hg_prepare_aggregate_msg": (_I, [_P, _P, _SZ]),
+    "hg_set_aggregate_level": (_I, [_P, _I]),
+    "hg_set_table_budget": (_I, [_P, _SZ]),
+    "hg_registry_non_g2": (_SZ, [_P]),
     "hg_set_message": (_I, [_P, _P, _SZ]),
     "hg_verify_batch": (_I, [_P, _P, _P, _SZ, _P]),
     "hg_verify_batch_msg": (_I, [_P, _P, _SZ, _P, _P, _SZ, _P]),

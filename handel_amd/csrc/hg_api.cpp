@@ -183,6 +183,16 @@ struct hg_ctx {
   // raised by hg_prepare_aggregate or by request volume (gt_requests).
   int gt_level = 0;
   size_t gt_requests = 0;
+  // -1: the volume policy; 0..2: every aggregate submission at that level
+  // (hg_set_aggregate_level; HG_GT_LEVEL / HG_AGG_PATH give the default)
+  int pinned_level = -1;
+  // highest level this registry may use: lowered when the device (or the
+  // table budget) could not hold a level's tables, reset by a registry load
+  int gt_cap = 2;
+  size_t table_budget = SIZE_MAX;  // bytes of GT tables (hg_set_table_budget)
+  // registry keys on the twist but outside G2 (go flavor only: x/crypto's
+  // Unmarshal accepts them); any such key pins the registry to level 0
+  size_t reg_non_g2 = 0;
   DevBuf<Gt> gt_key, gt_w8, gt_win, gt_blk;  // gt_w8: 8-key windows, gt_win: 16-key windows
   GtBlockIndex gt_bi{};
   // GT fold workspaces
@@ -218,6 +228,27 @@ static hipError_t end(hg_ctx* c, hipStream_t s) {
   c->last_s = s;
   return hipEventRecord(c->last_ev, s);
 }
+// One submission: end() runs on every exit once start() succeeded, error
+// returns included, so a later submission on another stream still waits for
+// whatever this one had queued.
+struct Submission {
+  hg_ctx* c;
+  hipStream_t s;
+  bool open = false;
+  Submission(hg_ctx* c_, hipStream_t s_) : c(c_), s(s_) {}
+  hipError_t start() {
+    hipError_t e = begin(c, s);
+    open = e == hipSuccess;
+    return e;
+  }
+  hipError_t finish() {
+    open = false;
+    return end(c, s);
+  }
+  ~Submission() {
+    if (open) (void)end(c, s);
+  }
+};
 
 // ---------------------------------------------------------------- timing
 struct PhaseTimer {
@@ -337,12 +368,13 @@ static int set_message_locked(hg_ctx* c, const uint8_t* msg, size_t len) {
     c->has_msg = true;
     return HG_ERR_HASH_EOF;
   }
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->d_k, k, sizeof k, hipMemcpyHostToDevice, c->stream));
   launch_hash_point(c->d_k, c->d_h, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   c->has_msg = true;
   return HG_OK;
@@ -355,7 +387,8 @@ static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uin
     return HG_ERR_ARG;
   }
   HG_CHECK(c, c->checks.ensure(n));
-  HG_CHECK(c, begin(c, s));
+  Submission sub(c, s);
+  HG_CHECK(c, sub.start());
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
   launch_decode_checks(d_pks, d_sigs, (int)n, c->flavor, c->checks.p, d_codes, s);
   if (c->hash_eof) k_fill_codes<<<nb(n), 256, 0, s>>>(d_codes, (int)n, HG_OK, HG_ERR_HASH_EOF);
@@ -363,7 +396,7 @@ static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uin
   all.stop();
   int rc = check_launch(c);
   if (rc) return rc;
-  HG_CHECK(c, end(c, s));
+  HG_CHECK(c, sub.finish());
   return HG_OK;
 }
 
@@ -372,13 +405,14 @@ static int verify_batch_host_locked(hg_ctx* c, const uint8_t* pks, const uint8_t
   HG_CHECK(c, c->bytes_a.ensure(n * 128));
   HG_CHECK(c, c->bytes_b.ensure(n * 64));
   HG_CHECK(c, c->codes_c.ensure(n));
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, pks, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
   int rc = verify_batch_device_locked(c, c->bytes_a.p, c->bytes_b.p, n, c->codes_c.p, c->stream);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -402,11 +436,19 @@ static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector
 // thresholds are those break-even volumes (a rent-or-buy rule: at most about
 // twice the cost of the better choice in hindsight). A message or registry
 // change drops the tables and restarts the count. hg_prepare_aggregate builds
-// the top level at once (serving). HG_GT_LEVEL=0/1/2 pins a level (0 = G2
-// fold only; tests and A/B runs); HG_AGG_PATH=g2 = 0.
+// the top level at once (serving). hg_set_aggregate_level pins a level per
+// context (0 = G2 fold only); HG_GT_LEVEL=0/1/2 (HG_AGG_PATH=g2 = 0) is the
+// pinned level of new contexts (tests and A/B runs).
+//
+// The tables are a cache, never a requirement: a level whose tables (or fold
+// workspaces) the device cannot hold, or that exceeds the context's table
+// budget, lowers the context's cap and the submission runs at the level below
+// (down to the G2 fold, which needs no tables). A registry with a key outside
+// G2 stays at level 0 (the GT product equals e(H, sum) only on G2).
 static constexpr size_t kGtMaxRegistry = 16384;
 static constexpr size_t kGtLevel1Requests = 16384;
 static constexpr size_t kGtLevel2Requests = (size_t)1 << 20;
+static constexpr int kNoMem = -1;  // internal: an allocation of the GT path failed (or is over budget)
 static int gt_forced_level() {
   static const int lvl = [] {
     const char* p = getenv("HG_AGG_PATH");
@@ -418,24 +460,62 @@ static int gt_forced_level() {
   }();
   return lvl;
 }
-static int gt_max_level(const hg_ctx* c) { return c->nreg <= kGtMaxRegistry ? 2 : 1; }
+static int gt_max_level(const hg_ctx* c) {
+  if (c->reg_non_g2) return 0;
+  const int top = c->nreg <= kGtMaxRegistry ? 2 : 1;
+  return top < c->gt_cap ? top : c->gt_cap;
+}
 
-// builds the tables up to `level` on stream s (inside a submission)
+// an allocation of the GT path: out of device memory -> kNoMem (the caller
+// falls back to a lower level), any other failure -> HG_ERR_DEVICE
+#define HG_GT_ALLOC(ctx, expr)                                                     \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ == hipErrorOutOfMemory) {                                               \
+      (void)hipGetLastError(); /* not sticky: keep it out of check_launch */       \
+      return kNoMem;                                                               \
+    }                                                                              \
+    if (e_ != hipSuccess) {                                                        \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return HG_ERR_DEVICE;                                                        \
+    }                                                                              \
+  } while (0)
+
+// bytes of the tables of `level` (cumulative) for an n-key registry
+static size_t gt_block_count(const hg_ctx* c, int* cnt) {
+  size_t total = 0;
+  for (int k = 4; k <= c->block_levels && k < 24; k++) {
+    const size_t v = (c->nreg + ((size_t)1 << k) - 1) >> k;
+    if (cnt) cnt[k] = (int)v;
+    total += v;
+  }
+  return total;
+}
+static size_t gt_table_bytes(const hg_ctx* c, int level) {
+  const size_t n = c->nreg, nwin8 = (n + 7) / 8, nwin16 = (n + 15) / 16;
+  size_t b = 0;
+  if (level >= 1) b += (n + nwin8 * 256 + gt_block_count(c, nullptr)) * sizeof(Gt);
+  if (level >= 2) b += nwin16 * 65536 * sizeof(Gt);
+  return b;
+}
+
+// builds the tables up to `level` on stream s (inside a submission); kNoMem
+// before any launch of the level that could not be held
 static int build_gt_locked(hg_ctx* c, hipStream_t s, int level) {
   const int n = (int)c->nreg;
   const int nwin8 = (n + 7) / 8, nwin16 = (n + 15) / 16;
   if (c->gt_level < 1 && level >= 1) {
-    HG_CHECK(c, c->gt_key.ensure(n));
-    HG_CHECK(c, c->gt_w8.ensure((size_t)nwin8 * 256));
-    // blocks of level k >= 4 (levels <= 3 are window entries)
+    if (gt_table_bytes(c, 1) > c->table_budget) return kNoMem;
     int cnt[24] = {0};
-    int total = 0;
+    const size_t total = gt_block_count(c, cnt);
+    int base = 0;
     for (int k = 4; k <= c->block_levels && k < 24; k++) {
-      cnt[k] = (int)(((size_t)n + ((size_t)1 << k) - 1) >> k);
-      c->gt_bi.base[k] = total;
-      total += cnt[k];
+      c->gt_bi.base[k] = base;
+      base += cnt[k];
     }
-    if (total) HG_CHECK(c, c->gt_blk.ensure(total));
+    HG_GT_ALLOC(c, c->gt_key.ensure(n));
+    HG_GT_ALLOC(c, c->gt_w8.ensure((size_t)nwin8 * 256));
+    if (total) HG_GT_ALLOC(c, c->gt_blk.ensure(total));
     launch_gt_keys(c->reg.p, n, c->d_lines, c->d_h, c->gt_key.p, s);
     launch_gt_windows8(c->gt_key.p, n, c->gt_w8.p, nwin8, s);
     for (int k = 4; k <= c->block_levels && k < 24; k++) {
@@ -447,7 +527,8 @@ static int build_gt_locked(hg_ctx* c, hipStream_t s, int level) {
     c->gt_level = 1;
   }
   if (c->gt_level < 2 && level >= 2) {
-    HG_CHECK(c, c->gt_win.ensure((size_t)nwin16 * 65536));
+    if (gt_table_bytes(c, 2) > c->table_budget) return kNoMem;
+    HG_GT_ALLOC(c, c->gt_win.ensure((size_t)nwin16 * 65536));
     launch_gt_windows16(c->gt_w8.p, nwin8, c->gt_win.p, nwin16, s);
     int rc = check_launch(c);
     if (rc) return rc;
@@ -456,49 +537,107 @@ static int build_gt_locked(hg_ctx* c, hipStream_t s, int level) {
   return HG_OK;
 }
 
+// caps the context's table level at `cap` and frees the tables above it
+static void gt_lower_cap(hg_ctx* c, int cap) {
+  if (cap < 0) cap = 0;
+  if (cap < c->gt_cap) c->gt_cap = cap;
+  if (c->gt_cap < 2) c->gt_win.release();
+  if (c->gt_cap < 1) {
+    c->gt_key.release();
+    c->gt_w8.release();
+    c->gt_blk.release();
+  }
+  if (c->gt_level > c->gt_cap) c->gt_level = c->gt_cap;
+}
+
 // the table level an aggregate submission of n requests runs at (counting
 // them towards the volume policy)
 static int gt_submission_level(hg_ctx* c, size_t n) {
   if (c->hash_eof || c->nreg == 0) return 0;
-  const int forced = gt_forced_level();
   const int top = gt_max_level(c);
-  if (forced >= 0) return forced < top ? forced : top;
+  if (c->pinned_level >= 0) return c->pinned_level < top ? c->pinned_level : top;
   c->gt_requests += n;
   int want = c->gt_requests >= kGtLevel2Requests ? 2 : (c->gt_requests >= kGtLevel1Requests ? 1 : 0);
   if (want < c->gt_level) want = c->gt_level;
   return want < top ? want : top;
 }
 
-// GT fold workspaces for n requests: a request's folded mask has at most
-// 4 nonzero 16-bit windows per registry-aligned 64-bit word, plus the block term
-// fold schedule: terms per chunk and k_gt_chunks workgroups (HG_GT_CHUNK /
-// HG_GT_GRID override them for tuning runs)
+// GT fold workspaces. A request of b bits has at most 8 nonzero 8-bit (4
+// 16-bit) windows per registry-aligned 64-bit word of its range, plus the
+// block term of a complemented fold.
+// Fold schedule: terms per chunk and k_gt_chunks workgroups (HG_GT_CHUNK /
+// HG_GT_GRID override them for tuning runs).
 static int env_int(const char* name, int def, int lo, int hi) {
   const char* e = getenv(name);
   const int v = e ? atoi(e) : def;
   return v >= lo && v <= hi ? v : def;
 }
-static int ensure_gt_fold(hg_ctx* c, size_t n, GtWork& w) {
+static int gt_chunk() {
   static const int chunk = env_int("HG_GT_CHUNK", kGtChunk, 1, 64);
+  return chunk;
+}
+static size_t fold_terms_bound(size_t bitlen) { return 8 * ((bitlen + 7 + 63) / 64) + 1; }
+// capacity of a batch's term and chunk lists
+struct FoldCaps {
+  size_t terms = 0, chunks = 0;
+  void add(size_t bitlen) {
+    const size_t m = fold_terms_bound(bitlen);
+    terms += m;
+    chunks += (m + gt_chunk() - 1) / gt_chunk();
+  }
+};
+// device-resident requests: their sizes are unknown on the host, every
+// request is bounded by the registry
+static FoldCaps fold_caps_worst(const hg_ctx* c, size_t n) {
+  FoldCaps one;
+  one.add(c->nreg);
+  FoldCaps all;
+  all.terms = one.terms * n;
+  all.chunks = one.chunks * n;
+  return all;
+}
+static int ensure_gt_fold(hg_ctx* c, size_t n, const FoldCaps& caps, GtWork& w) {
   static const int grid = env_int("HG_GT_GRID", 4096, 64, 65536);
-  const size_t mmax = 8 * ((c->nreg + 7 + 63) / 64 + 1) + 1;  // nonzero 8-key windows + the block term
-  const size_t cmax = (mmax + chunk - 1) / chunk;
-  HG_CHECK(c, c->gt_plan.ensure(n));
-  HG_CHECK(c, c->gt_hdr.ensure(1));
-  HG_CHECK(c, c->gt_terms.ensure(n * mmax));
-  HG_CHECK(c, c->gt_ord.ensure(n * cmax));
-  HG_CHECK(c, c->gt_multi.ensure(2 * n));
-  HG_CHECK(c, c->gt_partial.ensure(n * cmax));
-  HG_CHECK(c, c->gt_y.ensure(n));
+  if (caps.chunks > (size_t)INT32_MAX || caps.terms > (size_t)INT32_MAX) return kNoMem;
+  HG_GT_ALLOC(c, c->gt_plan.ensure(n));
+  HG_GT_ALLOC(c, c->gt_hdr.ensure(1));
+  HG_GT_ALLOC(c, c->gt_terms.ensure(caps.terms));
+  HG_GT_ALLOC(c, c->gt_ord.ensure(caps.chunks));
+  HG_GT_ALLOC(c, c->gt_multi.ensure(2 * n));
+  HG_GT_ALLOC(c, c->gt_partial.ensure(caps.chunks));
+  HG_GT_ALLOC(c, c->gt_y.ensure(n));
   w.plan = c->gt_plan.p;
   w.hdr = c->gt_hdr.p;
   w.terms = c->gt_terms.p;
   w.ord = c->gt_ord.p;
-  w.cap = (int)(n * cmax);
+  w.cap = (int)caps.chunks;
   w.multi = c->gt_multi.p;
   w.partial = c->gt_partial.p;
   w.chunk_grid = grid;
-  w.chunk = chunk;
+  w.chunk = gt_chunk();
+  return HG_OK;
+}
+
+// The tables of `level` and the fold workspaces of one submission (inside it,
+// on stream s). Lowers `level` for what the device cannot hold: tables that do
+// not fit cap the context (tables never get smaller for this registry), fold
+// workspaces that do not fit send this submission to the G2 fold only.
+static int gt_acquire(hg_ctx* c, hipStream_t s, size_t n, const FoldCaps& caps, int& level, GtWork& w) {
+  while (level > 0) {
+    int rc = c->gt_level < level ? build_gt_locked(c, s, level) : HG_OK;
+    if (rc == kNoMem) {
+      gt_lower_cap(c, c->gt_level < level ? c->gt_level : level - 1);
+      level = level < c->gt_cap ? level : c->gt_cap;
+      continue;
+    }
+    if (rc) return rc;
+    rc = ensure_gt_fold(c, n, caps, w);
+    if (rc == kNoMem) {
+      level = 0;
+      break;
+    }
+    return rc;
+  }
   return HG_OK;
 }
 
@@ -512,24 +651,28 @@ __global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t
 
 // The Combine fold and (verify) the pairing check of n requests, device
 // pointers, on stream s; d_lvl holds the level codes and is updated in place
-// (nullptr: computed here when the flow needs them).
+// (nullptr: computed here when the flow needs them). caps: the fold's list
+// capacities (nullptr: bounded by the registry size).
 static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
                                    const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
-                                   bool verify, hipStream_t s) {
+                                   bool verify, hipStream_t s, const FoldCaps* caps = nullptr) {
   if (verify && !c->has_msg) {
     c->err = "hg_set_message was not called";
     return HG_ERR_ARG;
   }
+  Submission sub(c, s);
+  HG_CHECK(c, sub.start());
   // GT path: the verdict needs no aggregate key in G2; the G2 fold still runs
   // when the caller wants the aggregate keys' marshals
-  const int level = verify ? gt_submission_level(c, n) : 0;
-  const bool use_gt = level > 0;
-  const bool g2_fold = !use_gt || d_agg;
+  int level = verify ? gt_submission_level(c, n) : 0;
   GtWork gw{};
-  if (use_gt) {
-    int rc = ensure_gt_fold(c, n, gw);
+  if (level > 0) {
+    const FoldCaps fc = caps ? *caps : fold_caps_worst(c, n);
+    int rc = gt_acquire(c, s, n, fc, level, gw);
     if (rc) return rc;
   }
+  const bool use_gt = level > 0;
+  const bool g2_fold = !use_gt || d_agg;
   if (g2_fold) {
     HG_CHECK(c, c->checks.ensure(n));
     HG_CHECK(c, c->order.ensure(n));
@@ -540,11 +683,6 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   if (verify) {
     HG_CHECK(c, c->pts1.ensure(n));
     HG_CHECK(c, c->codes_b.ensure(n));
-  }
-  HG_CHECK(c, begin(c, s));
-  if (use_gt && c->gt_level < level) {
-    int rc = build_gt_locked(c, s, level);
-    if (rc) return rc;
   }
   gw.win_bits = level == 2 ? 16 : 8;
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
@@ -563,7 +701,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     all.stop();
     int rc = check_launch(c);
     if (rc) return rc;
-    HG_CHECK(c, end(c, s));
+    HG_CHECK(c, sub.finish());
     return HG_OK;
   }
   if (!d_lvl) {
@@ -597,7 +735,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   all.stop();
   int rc = check_launch(c);
   if (rc) return rc;
-  HG_CHECK(c, end(c, s));
+  HG_CHECK(c, sub.finish());
   return HG_OK;
 }
 
@@ -606,11 +744,14 @@ static int aggregate_host_locked(hg_ctx* c, const hg_request* reqs, size_t n, co
   HG_CHECK(c, hipSetDevice(c->device));
   std::vector<int32_t> lvl;
   level_codes(c, reqs, n, lvl);
+  FoldCaps caps;  // exact bounds: the host knows every request's size
   for (size_t i = 0; i < n; i++) {
-    if (lvl[i] == HG_OK && (size_t)reqs[i].word_offset + (reqs[i].bitlen + 63) / 64 > nwords) {
+    if (lvl[i] != HG_OK) continue;
+    if ((size_t)reqs[i].word_offset + (reqs[i].bitlen + 63) / 64 > nwords) {
       c->err = "request words out of range";
       return HG_ERR_ARG;
     }
+    caps.add(reqs[i].bitlen);
   }
   HG_CHECK(c, c->reqs.ensure(n));
   HG_CHECK(c, c->words.ensure(nwords ? nwords : 1));
@@ -622,17 +763,18 @@ static int aggregate_host_locked(hg_ctx* c, const hg_request* reqs, size_t n, co
     d_agg = c->bytes_a.p;
   }
   if (verify) HG_CHECK(c, c->bytes_b.ensure(n * 64));
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->reqs.p, reqs, n * sizeof(hg_request), hipMemcpyHostToDevice, c->stream));
   if (nwords) HG_CHECK(c, hipMemcpyAsync(c->words.p, words, nwords * 8, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->codes_c.p, lvl.data(), n * 4, hipMemcpyHostToDevice, c->stream));
   if (verify) HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
   int rc = aggregate_device_locked(c, c->reqs.p, n, c->words.p, verify ? c->bytes_b.p : nullptr, c->codes_a.p, d_agg,
-                                   c->codes_c.p, verify, c->stream);
+                                   c->codes_c.p, verify, c->stream, &caps);
   if (rc) return rc;
   if (agg_out) HG_CHECK(c, hipMemcpyAsync(agg_out, d_agg, n * 128, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipMemcpyAsync(codes, verify ? c->codes_a.p : c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   if (agg_out) {
     // the reference has no aggregate for level errors / empty bitsets: zero them
@@ -653,14 +795,15 @@ static int sign_locked(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* 
   HG_CHECK(c, c->bytes_a.ensure(n * 64));
   HG_CHECK(c, c->bytes_b.ensure(n * 32));
   HG_CHECK(c, c->pts1.ensure(n));
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
   launch_g1_mul(c->d_h, c->bytes_b.p, (int)n, c->pts1.p, c->stream);
   launch_encode_g1(c->pts1.p, (int)n, c->bytes_a.p, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(sigs_out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -708,6 +851,7 @@ int hg_create(int device, int flavor, hg_ctx** out) {
   hg_ctx* c = new hg_ctx();
   c->device = device;
   c->flavor = flavor;
+  c->pinned_level = gt_forced_level();
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->d_lines, sizeof(LineCoef) * kNumLines);
@@ -764,7 +908,10 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   c->block_levels = 0;
   c->gt_level = 0;
   c->gt_requests = 0;
-  HG_CHECK(c, begin(c, c->stream));
+  c->gt_cap = 2;
+  c->reg_non_g2 = 0;
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   HG_CHECK(c, c->reg.ensure(n));
   HG_CHECK(c, c->bytes_a.ensure(n * 128));
@@ -782,6 +929,17 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   if (bad) {
     c->err = "registry contains keys that fail to unmarshal";
     return HG_ERR_PK_UNMARSHAL;
+  }
+  // go flavor: x/crypto accepts any on-twist key (bn256/go/bn256.go:113-120);
+  // count the keys outside G2 (cf rejected them in the decode above)
+  size_t non_g2 = 0;
+  if (c->flavor == HG_FLAVOR_GO && n) {
+    launch_g2_subgroup(c->reg.p, (int)n, c->codes_a.p, c->stream);
+    rc = check_launch(c);
+    if (rc) return rc;
+    HG_CHECK(c, hipMemcpyAsync(h.data(), c->codes_a.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HG_CHECK(c, hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < n; i++) non_g2 += h[i] != 0;
   }
   // sums of the aligned power-of-two blocks (Handel's level ranges), level by level
   int K = 0;
@@ -810,32 +968,78 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
     rc = check_launch(c);
     if (rc) return rc;
   }
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   c->block_levels = K;
   c->nreg = n;
+  c->reg_non_g2 = non_g2;
+  return HG_OK;
+}
+
+static int prepare_aggregate_locked(hg_ctx* c) {
+  if (!c->has_msg || c->nreg == 0) {
+    c->err = "hg_prepare_aggregate: needs a message and a registry";
+    return HG_ERR_ARG;
+  }
+  if (c->hash_eof) return HG_ERR_HASH_EOF;
+  int level = gt_max_level(c);
+  if (c->pinned_level >= 0 && c->pinned_level < level) level = c->pinned_level;
+  if (c->gt_level >= level) return HG_OK;
+  HG_CHECK(c, hipSetDevice(c->device));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
+  // the highest level the device (and the table budget) can hold
+  while (level > c->gt_level) {
+    int rc = build_gt_locked(c, c->stream, level);
+    if (rc == kNoMem) {
+      gt_lower_cap(c, c->gt_level < level ? c->gt_level : level - 1);
+      level = level < c->gt_cap ? level : c->gt_cap;
+      continue;
+    }
+    if (rc) return rc;
+  }
+  HG_CHECK(c, sub.finish());
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
 
 int hg_prepare_aggregate(hg_ctx* c) {
   if (!c) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  if (!c->has_msg || c->nreg == 0) {
-    c->err = "hg_prepare_aggregate: needs a message and a registry";
-    return HG_ERR_ARG;
-  }
-  if (c->hash_eof) return HG_ERR_HASH_EOF;
-  const int forced = gt_forced_level();
-  int level = gt_max_level(c);
-  if (forced >= 0 && forced < level) level = forced;
-  if (c->gt_level >= level) return HG_OK;
-  HG_CHECK(c, hipSetDevice(c->device));
-  HG_CHECK(c, begin(c, c->stream));
-  int rc = build_gt_locked(c, c->stream, level);
+  return prepare_aggregate_locked(c);
+}
+
+int hg_prepare_aggregate_msg(hg_ctx* c, const uint8_t* msg, size_t len) {
+  if (!c || (!msg && len)) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  int rc = set_message_locked(c, msg, len);
   if (rc) return rc;
-  HG_CHECK(c, end(c, c->stream));
-  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return prepare_aggregate_locked(c);
+}
+
+int hg_set_aggregate_level(hg_ctx* c, int level) {
+  if (!c || level < -1 || level > 2) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->pinned_level = level;
   return HG_OK;
+}
+
+int hg_set_table_budget(hg_ctx* c, size_t bytes) {
+  if (!c) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->table_budget = bytes;
+  // drop the built tables the new budget no longer covers; the cap is
+  // re-evaluated against the budget by the next build
+  if (c->gt_level >= 1 && gt_table_bytes(c, c->gt_level) > bytes)
+    gt_lower_cap(c, gt_table_bytes(c, 1) <= bytes ? 1 : 0);
+  c->gt_cap = 2;
+  return HG_OK;
+}
+
+size_t hg_registry_non_g2(hg_ctx* c) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  return c->reg_non_g2;
 }
 
 int hg_aggregate_tables(hg_ctx* c) {
@@ -866,11 +1070,12 @@ int hg_pack_verdicts_device(hg_ctx* c, const int32_t* d_codes, size_t n, uint8_t
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  HG_CHECK(c, begin(c, s));
+  Submission sub(c, s);
+  HG_CHECK(c, sub.start());
   launch_pack_verdicts(d_codes, (int)n, d_bits, s);
   int rc = check_launch(c);
   if (rc) return rc;
-  HG_CHECK(c, end(c, s));
+  HG_CHECK(c, sub.finish());
   return HG_OK;
 }
 
@@ -956,7 +1161,8 @@ int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   HG_CHECK(c, c->codes_a.ensure(n));
   HG_CHECK(c, c->codes_b.ensure(n));
   HG_CHECK(c, c->codes_c.ensure(n));
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, a, n * 64, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, b, n * 64, hipMemcpyHostToDevice, c->stream));
   launch_decode_g1(c->bytes_a.p, (int)n, c->flavor, c->pts1.p, c->codes_a.p, c->stream);
@@ -967,7 +1173,7 @@ int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -983,7 +1189,8 @@ int hg_combine_g2(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   HG_CHECK(c, c->codes_b.ensure(n));
   HG_CHECK(c, c->codes_c.ensure(n));
   uint8_t* d = c->bytes_a.p;
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(d, a, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(d + n * 128, b, n * 128, hipMemcpyHostToDevice, c->stream));
   launch_decode_g2(d, (int)n, c->flavor, c->pts2.p, c->codes_a.p, c->stream);
@@ -995,7 +1202,7 @@ int hg_combine_g2(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, d, n * 128, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -1012,7 +1219,8 @@ int hg_pair(hg_ctx* c, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t
   HG_CHECK(c, c->codes_a.ensure(n));
   HG_CHECK(c, c->codes_b.ensure(n));
   HG_CHECK(c, c->codes_c.ensure(n));
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, g2s, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, g1s, n * 64, hipMemcpyHostToDevice, c->stream));
   launch_decode_g2(c->bytes_a.p, (int)n, HG_FLAVOR_GO, c->pts2.p, c->codes_a.p, c->stream);
@@ -1023,7 +1231,7 @@ int hg_pair(hg_ctx* c, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(gt_out, c->bytes_a.p, n * 384, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -1036,14 +1244,15 @@ int hg_keygen(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* pks_out) 
   HG_CHECK(c, c->bytes_a.ensure(n * 128));
   HG_CHECK(c, c->bytes_b.ensure(n * 32));
   HG_CHECK(c, c->pts2.ensure(n));
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
   launch_g2_mul_base(c->bytes_b.p, (int)n, c->pts2.p, c->stream);
   launch_encode_g2(c->pts2.p, (int)n, c->bytes_a.p, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(pks_out, c->bytes_a.p, n * 128, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -1069,14 +1278,15 @@ int hg_debug_fp12(hg_ctx* c, int op, const uint8_t* a, const uint8_t* b, size_t 
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 384 * 3));
   uint8_t* d = c->bytes_a.p;
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(d, a, n * 384, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(d + n * 384, b, n * 384, hipMemcpyHostToDevice, c->stream));
   launch_fp12_op(op, d, d + n * 384, (int)n, d + 2 * n * 384, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, d + 2 * n * 384, n * 384, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
@@ -1135,14 +1345,15 @@ int hg_debug_fp_mul(hg_ctx* c, const uint32_t* a, const uint32_t* b, size_t n, u
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 32 * 3));
   uint32_t* da = (uint32_t*)c->bytes_a.p;
-  HG_CHECK(c, begin(c, c->stream));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(da, a, n * 32, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(da + 8 * n, b, n * 32, hipMemcpyHostToDevice, c->stream));
   launch_fp_mul(da, da + 8 * n, (int)n, da + 16 * n, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, da + 16 * n, n * 32, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, end(c, c->stream));
+  HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }

@@ -89,6 +89,26 @@ class Engine:
         return self._check(self.L.hg_prepare_aggregate(self.ctx), "hg_prepare_aggregate",
                            ok=(0, _lib.HG_ERR_HASH_EOF))
 
+    def prepare_aggregate_msg(self, msg: bytes) -> int:
+        """set_message + prepare_aggregate under one lock hold
+        (hg_prepare_aggregate_msg); HG_OK or HG_ERR_HASH_EOF."""
+        m = _u8(msg)
+        return self._check(self.L.hg_prepare_aggregate_msg(self.ctx, _ptr(m) if len(m) else None, len(m)),
+                           "hg_prepare_aggregate_msg", ok=(0, _lib.HG_ERR_HASH_EOF))
+
+    def set_aggregate_level(self, level: int) -> None:
+        """Pins the GT table level of aggregate submissions (0..2) or returns
+        them to the volume policy (-1) (hg_set_aggregate_level)."""
+        self._check(self.L.hg_set_aggregate_level(self.ctx, int(level)), "hg_set_aggregate_level")
+
+    def set_table_budget(self, nbytes: int) -> None:
+        """Upper bound for this context's GT tables (hg_set_table_budget)."""
+        self._check(self.L.hg_set_table_budget(self.ctx, int(nbytes)), "hg_set_table_budget")
+
+    def registry_non_g2(self) -> int:
+        """Registry keys on the twist but outside G2 (hg_registry_non_g2)."""
+        return int(self.L.hg_registry_non_g2(self.ctx))
+
     def aggregate_tables(self) -> int:
         """Table level aggregate requests run at (hg_aggregate_tables): 0 = G2
         fold, 1 = GT fold over 8-key windows, 2 = over 16-key windows."""

@@ -152,9 +152,32 @@ int hg_verify_multisig(hg_ctx* ctx, const uint32_t* bitlens, const uint32_t* wor
  * registry. HG_OK; HG_ERR_HASH_EOF (message cannot be hashed: nothing to
  * build); HG_ERR_ARG without a message or registry. Synchronous. */
 int hg_prepare_aggregate(hg_ctx* ctx);
+/* hg_set_message + hg_prepare_aggregate under ONE lock hold, so a concurrent
+ * caller with another message cannot take the tables in between (the Go
+ * PrepareAggregate, bn256/go/bn256.go:210-218: H is fixed per Handel run). */
+int hg_prepare_aggregate_msg(hg_ctx* ctx, const uint8_t* msg, size_t len);
 /* The table level aggregate requests currently run at: 0 = G2 point fold and
- * two-pairing check, 1 = GT fold over 8-key windows, 2 = over 16-key windows. */
+ * two-pairing check, 1 = GT fold over 8-key windows, 2 = over 16-key windows.
+ * The tables are a cache: a level the device cannot hold (or that exceeds the
+ * table budget) is skipped and requests run at the level below, down to 0.
+ * A go-flavor registry holding a key outside G2 stays at 0 (see
+ * hg_registry_non_g2). */
 int hg_aggregate_tables(hg_ctx* ctx);
+/* Pins the table level of this context's aggregate submissions (0..2, capped
+ * as above) or, with -1, returns them to the volume policy. New contexts take
+ * HG_GT_LEVEL / HG_AGG_PATH=g2 (= 0) from the environment, else -1. */
+int hg_set_aggregate_level(hg_ctx* ctx, int level);
+/* Upper bound in bytes for this context's GT tables (default: unlimited, the
+ * device's free memory decides). Processes sharing one GPU (simul's P
+ * processes x k instances, simul/node/main.go:63-131) give each context a
+ * share; level-2 tables take ~1.97 MB per key, level 1 ~15 kB per key. */
+int hg_set_table_budget(hg_ctx* ctx, size_t bytes);
+/* Keys of the loaded registry that lie on the twist but outside the order-n
+ * subgroup G2. x/crypto's G2.Unmarshal accepts them (bn256/go/bn256.go:113-120;
+ * cloudflare rejects them at load). The GT product e(H, pk_1)...e(H, pk_k)
+ * equals the reference's e(H, pk_1 + ... + pk_k) only on G2, so a registry
+ * with such keys is served by the G2 fold and the two-pairing check. */
+size_t hg_registry_non_g2(hg_ctx* ctx);
 
 /* Device-resident variant (reqs, words, sigs, codes, agg out on the device). */
 int hg_verify_aggregate_device(hg_ctx* ctx, const hg_request* d_reqs, size_t n, const uint64_t* d_words,

@@ -274,6 +274,15 @@ def f12_marshal(a):
     return bytes(out)
 
 
+def f12_unmarshal(b: bytes):
+    """Inverse of f12_marshal (x/crypto GT.Unmarshal order, no checks)."""
+    order = [5, 3, 1, 4, 2, 0]
+    c = [None] * 6
+    for i, k in enumerate(order):
+        c[k] = (int.from_bytes(b[64 * i:64 * i + 32], "big"), int.from_bytes(b[64 * i + 32:64 * i + 64], "big"))
+    return c
+
+
 # ---------------------------------------------------------------------------
 # Curve points in Jacobian form (x, y, z); infinity has z == 0
 # Group law follows x/crypto curve.go / twist.go (add-2007-bl with the
@@ -447,6 +456,41 @@ def g1_unmarshal(m: bytes, flavor: str = "go"):
     if not g1_on_curve(x, y):
         return None, ERR_CF_MALFORMED
     return (x, y), None
+
+
+def f2_sqrt(a):
+    """A square root in Fp2 = Fp[i]/(i^2 + 1) of a = (x, y) = x i + y, or None
+    (p = 3 mod 4: the norm's root, then the half-trace's; test infrastructure
+    for crafting twist points outside G2)."""
+    ax, ay = a[0] % P, a[1] % P
+    if ax == 0 and ay == 0:
+        return F2_ZERO
+    e = (P + 1) // 4
+    norm = (ax * ax + ay * ay) % P
+    nr = pow(norm, e, P)
+    if nr * nr % P != norm:
+        return None
+    half = pow(2, P - 2, P)
+    for d in ((ay + nr) * half % P, (ay - nr) * half % P):
+        c = pow(d, e, P)
+        if c * c % P != d:
+            continue
+        if c == 0:
+            # a = x i with y^2 = -x: root (x', 0) with -x'^2 = ay ... handled by the check below
+            cand = (pow(-ay % P, e, P), 0)
+        else:
+            cand = (ax * pow(2 * c, P - 2, P) % P, c)
+        if f2_sqr(cand) == (ax, ay):
+            return cand
+    return None
+
+
+def twist_point(x):
+    """The twist point (x, y) with y = sqrt(x^3 + b') (either root), or None
+    when x^3 + b' is not a square in Fp2."""
+    rhs = f2_add(f2_mul(f2_sqr(x), x), TWIST_B)
+    y = f2_sqrt(rhs)
+    return None if y is None else ((x[0] % P, x[1] % P), y)
 
 
 def g2_in_subgroup(a) -> bool:

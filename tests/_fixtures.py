@@ -74,3 +74,17 @@ def pack_requests(ranges, bitsets):
 
 def digest(b: bytes) -> str:
     return hashlib.sha256(b).hexdigest()
+
+
+def non_g2_points(k: int, seed: int = 1) -> list:
+    """k twist points outside the order-n subgroup G2 (random x, y = sqrt(x^3 + b')):
+    keys x/crypto's G2.Unmarshal accepts (bn256/go/bn256.go:113-120) and
+    cloudflare's rejects."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < k:
+        x = (int.from_bytes(rng.bytes(32), "big") % O.P, int.from_bytes(rng.bytes(32), "big") % O.P)
+        q = O.twist_point(x)
+        if q is not None and not O.g2_in_subgroup(q):
+            out.append(q)
+    return out

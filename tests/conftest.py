@@ -7,10 +7,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# Aggregate requests in the GPU suite run on the headline path (GT fold over
-# 16-key windows) whatever their volume; tests of the other table levels and
-# of the volume policy run in child processes with their own HG_GT_LEVEL.
-os.environ.setdefault("HG_GT_LEVEL", "2")
+# The session engines pin aggregate requests to the headline path (GT fold
+# over 16-key windows, hg_set_aggregate_level) whatever their volume; the
+# parity tests that matter at every level take the `agg_level` fixture (the
+# G2 fold + two-pairing check that serves a message's first requests by
+# default, and the GT path), and the volume policy itself is tested on
+# contexts left at the policy (level -1).
+AGG_LEVEL_DEFAULT = 2
 
 
 def pytest_configure(config):
@@ -32,6 +35,7 @@ def engine():
     from handel_amd.engine import Engine
     _torch_first()
     e = Engine(device=0, flavor="go")
+    e.set_aggregate_level(AGG_LEVEL_DEFAULT)
     yield e
     e.close()
 
@@ -41,5 +45,20 @@ def engine_cf():
     from handel_amd.engine import Engine
     _torch_first()
     e = Engine(device=0, flavor="cf")
+    e.set_aggregate_level(AGG_LEVEL_DEFAULT)
     yield e
     e.close()
+
+
+@pytest.fixture(params=[0, 2], ids=["g2fold", "gt16"])
+def agg_level(request):
+    """Runs an aggregate parity test at table level 0 (G2 point fold +
+    two-pairing k_verify: a message's first 16384 requests by default) and at
+    level 2 (GT fold over 16-key windows + k_verify_sig: the serving path); the
+    session engines are pinned for the test and restored afterwards."""
+    engines = [request.getfixturevalue(n) for n in ("engine", "engine_cf")]
+    for e in engines:
+        e.set_aggregate_level(request.param)
+    yield request.param
+    for e in engines:
+        e.set_aggregate_level(AGG_LEVEL_DEFAULT)

@@ -1,0 +1,171 @@
+"""GPU suite: where the GT path may and may not serve a registry.
+
+The GT fold uses e(H, pk_1 + ... + pk_k) = e(H, pk_1) ... e(H, pk_k), which
+holds on the order-n subgroup G2 only. x/crypto's G2.Unmarshal accepts any
+point on the twist (bn256/go/bn256.go:113-120), so a go-flavor registry can
+hold keys outside G2; the reference then still folds them with
+PublicKey.Combine (processing.go:355-363) and pairs the sum
+(bn256/go/bn256.go:82-94). hg_registry_load detects such keys and keeps the
+registry on the G2 fold + two-pairing check, whose verdicts are the
+reference's. Also here: the GT tables as a cache under a memory budget (a
+level the context cannot hold is skipped, never an error).
+"""
+
+import numpy as np
+import pytest
+
+from handel_amd.engine import REQ_DTYPE
+from oracle import bn256_oracle as O
+from oracle import ref_lib as R
+from tests import _fixtures as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(msg, reg, reqs, words, sigs):
+    # fast=0: the reference algorithm itself (Combine fold, two pairings, GT byte compare)
+    return R.verify_aggregate(msg, reg, reqs["offset"], reqs["bitlen"], reqs["level_size"], words,
+                              reqs["word_offset"].astype(np.uint64), sigs, nthreads=8, fast=False)
+
+
+def _crafted_registry(n=64):
+    """n keys; keys 10, 11, 12 are A, B, C = -(A + B) with A, B twist points
+    outside G2 (so C is too): the three sum to infinity in the group, but
+    their GT values multiply to e(H,A) e(H,B) e(H,C) != 1."""
+    ks = F.scalars(n, seed=b"non-g2")
+    pts = [O.g2_mul(O.G2_GEN, k) for k in ks]
+    a, b = F.non_g2_points(2, seed=3)
+    c = O.g2_neg(O.g2_add(a, b))
+    pts[10], pts[11], pts[12] = a, b, c
+    for i in (10, 11, 12):
+        ks[i] = None
+    return ks, b"".join(O.g2_marshal(p) for p in pts)
+
+
+def test_non_g2_registry_keeps_reference_verdicts(engine):
+    """A go-flavor registry with keys outside G2: the context reports them,
+    stays at table level 0 even when prepared with level 2 pinned, and every
+    verdict equals the reference algorithm's, including the two requests whose
+    aggregate contains A + B + C = infinity (valid in the reference, invalid
+    in a GT-product fold, which the explicit GT product below demonstrates)."""
+    msg = F.LIB_MESSAGE
+    ks, reg = _crafted_registry()
+    assert list(engine.registry_load(reg)) == [0] * 64
+    assert engine.registry_non_g2() == 3
+    assert engine.set_message(msg) == 0
+    assert engine.prepare_aggregate() == 0
+    assert engine.aggregate_tables() == 0
+    h = O.hashed_message(msg)[0]
+
+    def sig_of(idx):
+        k = sum(ks[i] for i in idx) % O.ORDER
+        return O.g1_marshal(O.g1_mul(h, k)) if k else bytes(64)
+
+    honest = [i for i in range(64) if ks[i] is not None]
+    cases = [  # (offset, size, set bits (registry indices), signature)
+        (8, 8, [10, 11, 12], bytes(64)),                   # A + B + C = inf: sig inf is valid
+        (8, 8, [10, 11, 12], sig_of([8])),                 # ... any other sig is not
+        (0, 64, list(range(64)), sig_of(honest)),          # honest sum + (A + B + C): valid
+        (8, 8, [8, 9, 10, 11, 12, 13], sig_of([8, 9, 13])),  # the same inside a level block
+        (8, 8, [10], bytes(64)),                           # A alone
+        (8, 8, [10, 11], sig_of([9])),                     # A + B, some sig
+        (0, 8, [0, 3, 5], sig_of([0, 3, 5])),              # honest keys only
+        (32, 32, list(range(32, 64)), sig_of(range(32, 64))),
+    ]
+    ranges, bitsets, sigs = [], [], b""
+    for off, size, idx, sig in cases:
+        ranges.append((off, size))
+        b = [False] * size
+        for i in idx:
+            b[i - off] = True
+        bitsets.append(b)
+        sigs += sig
+    reqs, words = F.pack_requests(ranges, bitsets)
+    reqs = np.array(reqs, dtype=REQ_DTYPE)
+    want = _oracle(msg, reg, reqs, words, sigs)
+    assert list(want[[0, 2, 3, 6, 7]]) == [0, 0, 0, 0, 0] and want[1] == 1
+    got = engine.verify_aggregate(reqs, words, sigs)
+    assert list(got) == list(want)
+    codes, agg = engine.verify_aggregate(reqs, words, sigs, want_agg=True)
+    assert list(codes) == list(want)
+    _, want_agg = R.verify_aggregate(msg, reg, reqs["offset"], reqs["bitlen"], reqs["level_size"], words,
+                                     reqs["word_offset"].astype(np.uint64), sigs, nthreads=8, want_agg=True)
+    assert agg == want_agg
+    assert agg[:128] == bytes(128)  # A + B + C marshals as infinity
+    # why the GT fold may not serve this registry: the GT values of A, B, C do
+    # not multiply to 1 although the keys sum to infinity
+    hb = O.g1_marshal(h)
+    gts = [O.f12_unmarshal(R.pair(hb, reg[128 * i:128 * i + 128])) for i in (10, 11, 12)]
+    prod = O.f12_mul(O.f12_mul(gts[0], gts[1]), gts[2])
+    assert not O.f12_is_one(prod)
+
+
+def test_non_g2_registry_single_key_requests(engine):
+    """One-key requests on the crafted registry (the p2p aggregator's
+    verifyPacket shape, routed through the aggregate path by the Go shim):
+    the reference's verdict for the non-G2 keys with the infinity signature."""
+    msg = F.TEST_MESSAGES[0]
+    ks, reg = _crafted_registry()
+    assert list(engine.registry_load(reg)) == [0] * 64
+    assert engine.set_message(msg) == 0
+    h = O.hashed_message(msg)[0]
+    idx = [0, 10, 11, 12, 63]
+    sigs = b"".join(bytes(64) if ks[i] is None else O.g1_marshal(O.g1_mul(h, ks[i])) for i in idx)
+    reqs = np.array([(i, 1, 1, j) for j, i in enumerate(idx)], dtype=REQ_DTYPE)
+    words = np.ones(len(idx), dtype=np.uint64)
+    got = engine.verify_aggregate(reqs, words, sigs)
+    assert list(got) == list(_oracle(msg, reg, reqs, words, sigs))
+    assert got[0] == 0 and got[-1] == 0
+
+
+def test_non_g2_registry_rejected_by_cf(engine_cf):
+    """cloudflare's G2 unmarshal rejects the same keys (subgroup check), so the
+    cf context ends with no registry."""
+    _, reg = _crafted_registry()
+    codes = engine_cf.registry_load(reg)
+    assert [int(codes[i]) for i in (10, 11, 12)] == [8, 8, 8]  # bn256: malformed point
+    assert int(np.count_nonzero(codes)) == 3
+    assert engine_cf.registry_non_g2() == 0
+
+
+def test_g2_registry_reports_no_outliers(engine):
+    ks = F.scalars(40, seed=b"all-g2")
+    assert not engine.registry_load(R.g2_scalar_base(F.scalar_bytes(ks))).any()
+    assert engine.registry_non_g2() == 0
+    assert engine.set_message(F.LIB_MESSAGE) == 0
+    assert engine.prepare_aggregate() == 0
+    assert engine.aggregate_tables() == 2
+
+
+def test_table_budget_selects_the_level_that_fits(engine):
+    """hg_set_table_budget: level-2 tables of a 1000-key registry take ~2 GB
+    and level 1 ~16 MB. A 100 MB budget stops at level 1, a zero budget at the
+    G2 fold, an unlimited one builds level 2 — the verdicts are the same at
+    every level."""
+    import bench
+
+    assert engine.set_message(bench.LIB_MESSAGE) == 0
+    reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(engine, 1000, 512, seed=17)
+    try:
+        for budget, level in ((100 << 20, 1), (0, 0), ((1 << 64) - 1, 2), (100 << 20, 1)):
+            engine.set_table_budget(budget)
+            assert engine.prepare_aggregate() == 0
+            assert engine.aggregate_tables() == level, budget
+            assert np.array_equal(engine.verify_aggregate(reqs, words, sigs), expect), budget
+    finally:
+        engine.set_table_budget((1 << 64) - 1)
+    assert np.array_equal(_oracle(bench.LIB_MESSAGE, reg, reqs, words, sigs), expect)
+
+
+def test_prepare_aggregate_msg_one_lock_hold(engine):
+    """hg_prepare_aggregate_msg hashes and builds for the given message."""
+    ks = F.scalars(24, seed=b"prep-msg")
+    reg = R.g2_scalar_base(F.scalar_bytes(ks))
+    assert not engine.registry_load(reg).any()
+    assert engine.prepare_aggregate_msg(F.REJECT_MESSAGES[0]) == 2
+    assert engine.prepare_aggregate_msg(F.TEST_MESSAGES[2]) == 0
+    assert engine.aggregate_tables() == 2
+    h = O.hashed_message(F.TEST_MESSAGES[2])[0]
+    sig = O.g1_marshal(O.g1_mul(h, sum(ks[:8]) % O.ORDER))
+    reqs = np.array([(0, 8, 8, 0)], dtype=REQ_DTYPE)
+    assert list(engine.verify_aggregate(reqs, np.array([0xff], dtype=np.uint64), sig)) == [0]

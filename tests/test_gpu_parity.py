@@ -145,7 +145,7 @@ def test_combine_g1_matches_oracle(engine):
     assert out[4 * 64:5 * 64] == bytes(64)  # sig + (-sig) = infinity
 
 
-def test_verify_aggregate_matches_oracle(engine):
+def test_verify_aggregate_matches_oracle(engine, agg_level):
     n_reg = 50
     ks, reg, _ = F.keys_and_sigs(n_reg, seed=b"agg")
     msg = F.LIB_MESSAGE
@@ -192,7 +192,7 @@ def engine_req_dtype():
     return REQ_DTYPE
 
 
-def test_aggregate_block_complement_matches_oracle(engine):
+def test_aggregate_block_complement_matches_oracle(engine, agg_level):
     """Level ranges of a 300-key registry (aligned blocks, clipped last blocks,
     multi-word bitsets) at densities that take the block-sum complement path
     (all set, all but one, just over half) and the direct path (half, one bit),
@@ -242,7 +242,7 @@ def test_aggregate_block_complement_matches_oracle(engine):
         assert agg[128 * i:128 * (i + 1)] == want_agg[128 * i:128 * (i + 1)], f"agg {i} {ranges[i]}"
 
 
-def test_aggregate_unaligned_ranges_match_oracle(engine):
+def test_aggregate_unaligned_ranges_match_oracle(engine, agg_level):
     """Ranges that are not Handel level blocks (offsets off the 8-key window
     grid, lengths that straddle windows and words): the window subset-sum fold
     must shift the bitset into registry-aligned windows and never take the
@@ -305,7 +305,7 @@ def test_full_size_ragged_batch_matches_oracle(request, flavor):
 
 @pytest.mark.parametrize("flavor", ["go", "cf"])
 @pytest.mark.parametrize("full", [False, True], ids=["levels", "full_registry"])
-def test_full_size_aggregate_matches_oracle(request, full, flavor):
+def test_full_size_aggregate_matches_oracle(request, full, flavor, agg_level):
     """BASELINE config 3 at full size: 4096 multisigs on a 4000-key registry
     (random Handel levels, or VerifyMultiSignature over the whole registry),
     verdicts and aggregate-key marshals byte-exact against the C restatement,
@@ -317,8 +317,10 @@ def test_full_size_aggregate_matches_oracle(request, full, flavor):
     n, n_reg = 4096, 4000
     assert engine.set_message(F.LIB_MESSAGE) == 0
     reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(engine, n_reg, n, seed=77, full=full)
-    codes, agg = engine.verify_aggregate(reqs, words, sigs, want_agg=True)
+    codes = engine.verify_aggregate(reqs, words, sigs)  # verdicts only: the GT path alone at level 2
+    codes_a, agg = engine.verify_aggregate(reqs, words, sigs, want_agg=True)  # + the G2 fold for the keys
     assert np.array_equal(codes, expect)  # exactly the tampered 1/8 fail
+    assert np.array_equal(codes_a, expect)
     want, want_agg = R.verify_aggregate(F.LIB_MESSAGE, reg, reqs["offset"], reqs["bitlen"], reqs["level_size"],
                                         words, reqs["word_offset"].astype(np.uint64), sigs, nthreads=16,
                                         want_agg=True)
