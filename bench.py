@@ -196,16 +196,28 @@ def pmc_traffic(pattern: str):
     return None, None
 
 
+def _cgroup_quota_cpus():
+    """CPUs of CPU time the cgroup grants this process (cgroup v2 cpu.max
+    "quota period"), None when unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpu():
-    """(threads to use, description) — the box's CPU share for one GPU is the
-    thread budget (OMP_NUM_THREADS / the affinity mask), nproc and the model
-    are reported beside it."""
+    """(threads to use, description): every core the process can actually run
+    on — the affinity mask, capped by the cgroup's CPU quota when there is one
+    (a quota of 16 CPUs lets 256 threads run no faster than 16 cores).
+    OMP_NUM_THREADS is reported but not used."""
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         aff = os.cpu_count() or 1
-    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(aff, omp) if omp > 0 else aff
+    quota = _cgroup_quota_cpus()
+    threads = min(aff, max(1, int(quota + 0.999))) if quota else aff
     model = platform.processor() or "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -215,19 +227,31 @@ def host_cpu():
                     break
     except OSError:  # pragma: no cover
         pass
-    return threads, {"nproc": os.cpu_count(), "affinity": aff, "model": model}
+    return threads, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+                     "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
 
 
 def _host_scale(per_core: float, info: dict) -> dict:
-    """The box gives one GPU's job a CPU share (the threads measured); the
-    whole host's rate is extrapolated per core (linear: the checks are
-    independent), and so is one GPU's share of the host (nproc / 8 GPUs)."""
-    nproc = info.get("nproc") or 1
-    return {"host_all_cores_extrapolated": round(per_core * nproc, 1),
-            "host_share_per_gpu_extrapolated": round(per_core * nproc / 8, 1)}
+    """Extrapolations (never the measured value): the whole host's cores at the
+    measured per-core rate (the checks are independent), and one GPU's share
+    of them (8 GPUs per host)."""
+    cores = info.get("affinity") or info.get("nproc") or 1
+    return {"host_all_cores_extrapolated": round(per_core * cores, 1),
+            "host_share_per_gpu_extrapolated": round(per_core * cores / 8, 1)}
 
 
-def cpu_baseline_single(pks: bytes, sigs: bytes, expect: np.ndarray):
+def _timed_repeats(run, min_wall: float):
+    """Runs run() until min_wall seconds have passed; (calls, seconds)."""
+    calls, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        calls += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_wall:
+            return calls, dt
+
+
+def cpu_baseline_single(pks: bytes, sigs: bytes, expect: np.ndarray, min_wall: float = 3.0):
     """Config 2 on the reference algorithm restated in C (oracle/bn256_ref.c,
     'port'): two full pairings + GT compare per check."""
     from oracle import ref_lib as R
@@ -236,41 +260,59 @@ def cpu_baseline_single(pks: bytes, sigs: bytes, expect: np.ndarray):
     n = len(expect)
     R.set_rehash(True)  # hashedMessage on every check, as VerifySignature does
     try:
-        t0 = time.perf_counter()
         codes = R.verify_batch(LIB_MESSAGE, pks, sigs, nthreads=threads, fast=0)
-        dt = time.perf_counter() - t0
+        assert np.array_equal(codes, expect), "CPU oracle verdicts differ"
+        calls, dt = _timed_repeats(lambda: R.verify_batch(LIB_MESSAGE, pks, sigs, nthreads=threads, fast=0),
+                                   min_wall)
     finally:
         R.set_rehash(False)
-    assert np.array_equal(codes, expect), "CPU oracle verdicts differ"
-    return {"value": round(n / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
-            "per_core": round(n / dt / threads, 1), **info, **_host_scale(n / dt / threads, info),
-            "sample": f"the same {n} checks (lib.Message, 1/8 tampered), reference algorithm "
+    v = n * calls / dt
+    return {"value": round(v, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
+            "per_core": round(v / threads, 1), **info, **_host_scale(v / threads, info),
+            "sample": f"the same {n} checks (lib.Message, 1/8 tampered) x {calls}, reference algorithm "
                       f"(hashedMessage + 2 pairings + GT compare per check), {threads} threads, {dt:.2f} s wall"}
 
 
-def cpu_baseline_aggregate(reg: bytes, reqs, words, sigs: bytes, expect: np.ndarray, n_sample: int):
+def cpu_baseline_aggregate(reg: bytes, reqs, words, sigs: bytes, expect: np.ndarray, n_sample: int,
+                           min_wall: float = 3.0):
     """Config 3 on the reference algorithm restated in C: per request the
     PublicKey.Combine fold over every set bit (one G2 addition each, as
-    processing.go:355-363), then two pairings + GT compare."""
+    processing.go:355-363), then two pairings + GT compare. Measured on every
+    usable core for >= min_wall seconds (the sample repeated); when the
+    affinity mask holds more threads than the cgroup quota lets run, a second
+    measurement with one thread per affinity core shows what the whole mask
+    delivers."""
     from oracle import ref_lib as R
 
     threads, info = host_cpu()
     m = min(n_sample, len(reqs))
     r = reqs[:m]
+
+    def run(nt):
+        return R.verify_aggregate(LIB_MESSAGE, reg, r["offset"], r["bitlen"], r["level_size"], words,
+                                  r["word_offset"].astype(np.uint64), sigs[:64 * m], nthreads=nt, fast=0)
+
     R.set_rehash(True)  # hashedMessage on every check, as VerifySignature does
     try:
-        t0 = time.perf_counter()
-        codes = R.verify_aggregate(LIB_MESSAGE, reg, r["offset"], r["bitlen"], r["level_size"], words,
-                                   r["word_offset"].astype(np.uint64), sigs[:64 * m], nthreads=threads, fast=0)
-        dt = time.perf_counter() - t0
+        assert np.array_equal(run(threads), expect[:m]), "CPU oracle verdicts differ"
+        calls, dt = _timed_repeats(lambda: run(threads), min_wall)
+        aff_run = None
+        if info["affinity"] > threads:
+            acalls, adt = _timed_repeats(lambda: run(info["affinity"]), min_wall)
+            aff_run = {"threads": info["affinity"], "value": round(m * acalls / adt, 1), "wall_s": round(adt, 2),
+                       "note": "one thread per core of the affinity mask; the cgroup quota "
+                               f"({info['cgroup_quota_cpus']} CPUs) bounds what they can run"}
     finally:
         R.set_rehash(False)
-    assert np.array_equal(codes, expect[:m]), "CPU oracle verdicts differ"
-    return {"value": round(m / dt, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
-            "per_core": round(m / dt / threads, 1), **info, **_host_scale(m / dt / threads, info),
-            "sample": f"the first {m} requests of the batch (same registry, bitsets, signatures), reference "
-                      f"algorithm (one G2 addition per set bit + hashedMessage + 2 pairings + GT compare), {threads} threads, "
-                      f"{dt:.2f} s wall"}
+    v = m * calls / dt
+    out = {"value": round(v, 1), "unit": "verifications/s", "cores": threads, "kind": "port",
+           "per_core": round(v / threads, 1), **info, **_host_scale(v / threads, info),
+           "sample": f"the first {m} requests of the batch x {calls} (same registry, bitsets, signatures), reference "
+                     f"algorithm (one G2 addition per set bit + hashedMessage + 2 pairings + GT compare), "
+                     f"{threads} threads, {dt:.2f} s wall"}
+    if aff_run:
+        out["affinity_run"] = aff_run
+    return out
 
 
 class Timer:
@@ -308,7 +350,8 @@ def _dev_bytes(b: bytes, dev):
 class AggregateWorkload:
     """Config 3 (or 5): n multisignatures on an n_reg-key registry per rank."""
 
-    def __init__(self, eng: Engine, n_reg: int, n: int, seed: int, dev, stream, full: bool = False):
+    def __init__(self, eng: Engine, n_reg: int, n: int, seed: int, dev, stream, full: bool = False,
+                 prepare: bool = True):
         self.eng, self.n, self.stream = eng, n, stream
         (self.reqs, self.words, self.sigs, self.expect, self.signers,
          self.reg) = make_aggregate_batch(eng, n_reg, n, seed, full=full)
@@ -316,7 +359,8 @@ class AggregateWorkload:
         # (once per Handel run: the message and the registry are fixed)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        assert eng.prepare_aggregate() == 0
+        if prepare:
+            assert eng.prepare_aggregate() == 0
         self.setup_ms = (time.perf_counter() - t0) * 1e3
         self.terms = gt_fold_terms(self.reqs, self.words, n_reg)
         self.d_reqs = _dev_bytes(self.reqs.tobytes(), dev)
@@ -366,6 +410,45 @@ class SingleWorkload:
     def check(self):
         got = self.d_codes.cpu().numpy()
         assert np.array_equal(got, self.expect), f"GPU verdicts differ at {np.flatnonzero(got != self.expect)[:8]}"
+
+
+def handel_run_volume(dev, stream, device: int, n_reg: int = 2000, requests: int = 90112, batch: int = 4096,
+                      seed: int = 2468):
+    """A Handel run's verification volume on a FRESH (message, registry), the
+    table builds inside the timed region: config 4 is 2000 nodes x 45.2 checks
+    per node ~ 90 k requests of one message (simul/plots/csv/
+    handel_0failing_99thr.csv:7; H is fixed per run, bn256/go/bn256.go:210-218).
+    'policy': the engine's own volume policy (G2 fold first, the 8-key GT
+    tables once 16384 requests have come in); 'prepared': hg_prepare_aggregate
+    (the 16-key tables) first. The batch of 4096 config-4-shaped requests is
+    resubmitted requests/batch times (the policy counts requests)."""
+    out = {"requests": requests, "batch": batch, "registry": n_reg,
+           "workload": f"{n_reg}-key registry, random node/level, bitset density U[0.5,1], 1/8 tampered"}
+    for mode in ("policy", "prepared"):
+        e = Engine(device=device, flavor="go")
+        try:
+            e.set_aggregate_level(-1)
+            assert e.set_message(LIB_MESSAGE) == 0
+            wl = AggregateWorkload(e, n_reg, batch, seed=seed, dev=dev, stream=stream, prepare=False)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            assert not e.registry_load(wl.reg).any()  # a fresh registry: block/window sums, G2 membership
+            load_ms = (time.perf_counter() - t0) * 1e3
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            if mode == "prepared":
+                assert e.prepare_aggregate() == 0
+            for _ in range(requests // batch):
+                wl.submit(eng=e)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            wl.check()
+            out[mode] = {"ms": round(dt * 1e3, 3), "value": round(requests // batch * batch / dt, 1),
+                         "unit": "verifications/s", "tables_at_end": e.aggregate_tables()}
+            out["registry_load_ms"] = round(load_ms, 3)
+        finally:
+            e.close()
+    return out
 
 
 def timed_phases(eng: Engine, run):
@@ -456,18 +539,28 @@ def main():
         assert torch.equal(gathered[rank].cpu(), want[0]), "gathered bitset of this rank differs"
     ph = timed_phases(eng, lambda: [head.submit() for _ in range(5)])
     value = n * args.steps * world / dt
-    # the dominant kernels of the step: the Combine fold (plan, order, fold,
-    # finish) and the pairing check, on the reference's algorithmic work
-    agg_ms = ph["fold"] + ph["verify"]
-    roof = roofline(head.fpmul, agg_ms, "GT fold (k_gt_plan, k_gt_chunks, k_gt_combine) + k_verify_sig",
-                    r"k_gt_(plan|chunks|combine)|k_verify_sig",
-                    f"the REFERENCE algorithm's work per check (SURVEY.md 8(d)): {FPMUL_PER_G2_ADD} Fp-mul per set "
-                    f"bit (G2 addition) + {FPMUL_PER_CHECK} (two-pairing check), x {MADS_PER_FPMUL} u32 mads; mean "
-                    f"{head.signers.mean():.1f} set bits; the GT path runs less (roofline_k_verify, roofline_gt_fold)")
+    # the dominant kernels of the step: the GT fold (plan, chunks, combine) and
+    # the pairing check, on the work they implement (the primary roofline)
+    # (the fold runs on a side stream beside the pairing kernel: the
+    # submission's kernel time, prologue to comparison, is the time base)
+    agg_ms = ph["submit"]
+    impl_fpmul = head.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING
+    roof = roofline(impl_fpmul, agg_ms, "the GT submission: k_agg_prologue, k_verify_sig beside the GT fold "
+                    "(k_gt_plan, k_gt_chunks, k_gt_combine), k_gt_compare",
+                    r"k_agg_prologue|k_gt_(plan|chunks|combine|compare)|k_verify_sig",
+                    f"implemented work: {head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 "
+                    f"product each) + {n} x {FPMUL_PER_SIG_PAIRING} Fp-mul (one pairing + final exponentiation "
+                    f"per check), x {MADS_PER_FPMUL} u32 mads")
     roof["kernels_ms"] = {"fold": round(ph["fold"], 4), "k_verify": round(ph["verify"], 4),
                           "submit": round(ph["submit"], 4)}
-    # the kernels' own work (what the GT path runs): the pairing check kernel
-    # and the GT fold, each on its implemented algorithmic Fp-mul count
+    # the reference algorithm's work over the same time: a rate, not a
+    # utilisation (the GT path skips the G2 fold and the pk-side pairing)
+    effective = {"value": round(head.fpmul * MADS_PER_FPMUL / (agg_ms * 1e-3) / 1e12, 3),
+                 "unit": "Tmad/s of reference-algorithm work",
+                 "work": f"the REFERENCE algorithm per check (SURVEY.md 8(d)): {FPMUL_PER_G2_ADD} Fp-mul per set bit "
+                         f"(G2 addition) + {FPMUL_PER_CHECK} (two-pairing check), x {MADS_PER_FPMUL} u32 mads; mean "
+                         f"{head.signers.mean():.1f} set bits",
+                 "note": "work the GT path does not run is credited here; not a fraction of any peak"}
     roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph["verify"], "k_verify_sig", r"k_verify_sig",
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
                            "+ final exponentiation, oracle op count)")
@@ -493,7 +586,7 @@ def main():
             "value": round(n * args.steps * world / sdt, 1), "unit": "verifications/s",
             "ms_per_step": round(sdt / args.steps * 1e3, 4),
             "workload": f"config 2: {n} independent BLS pairing checks per GPU (lib.Message, 1/8 tampered)",
-            "roofline": roofline(single.fpmul, sph["verify"], "k_verify", r"k_verify",
+            "roofline": roofline(single.fpmul, sph["verify"], "k_verify", r"k_verify(?!_)",
                                  f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads per check")}
         if rank == 0 and world == 1 and not args.no_cpu:
             try:
@@ -540,8 +633,11 @@ def main():
                         "(crypto.go:120-137), bitset density U[0.5,1], 1/8 tampered",
             "signers_per_check_mean": round(float(full.signers.mean()), 1),
             "kernels_ms": {k: round(v, 4) for k, v in fph.items() if v is not None},
-            "roofline": roofline(full.fpmul, fph["fold"] + fph["verify"], "fold + k_verify",
-                                 r"k_agg_|k_aggregate|k_verify", "as the headline")}
+            "roofline": roofline(full.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING, fph["submit"],
+                                 "the GT submission (as the headline)",
+                                 r"k_agg_prologue|k_gt_(plan|chunks|combine|compare)|k_verify_sig",
+                                 f"implemented work: {full.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul + "
+                                 f"{n} x {FPMUL_PER_SIG_PAIRING} Fp-mul, x {MADS_PER_FPMUL} u32 mads")}
         del full
         # reload the headline registry (the full-registry workload replaced it)
         assert not eng.registry_load(head.reg).any()
@@ -570,6 +666,8 @@ def main():
                                   "note": "headline batch on each of the streams; throughput with batches overlapped"}
             for e in engs[1:]:
                 e.close()
+
+        extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -600,6 +698,7 @@ def main():
                        "signers_per_check_max": int(head.signers.max()),
                        "parallelism": f"dp{world} (one batch per GPU, RCCL all_gather of verdict bitsets)"},
             "roofline": roof,
+            "effective_rate": effective,
             "roofline_k_verify": roof_verify,
             "roofline_gt_fold": roof_fold,
             "setup": {"ms": round(head.setup_ms, 2), "what": "per (message, registry), outside the timed "
@@ -607,6 +706,7 @@ def main():
                       "block (hg_prepare_aggregate)",
                       "cold_value": round(n / ((head.setup_ms + dt / args.steps * 1e3) * 1e-3), 1)},
             "cpu_baseline": cpu,
+            "gpu_over_cpu": (round(value / cpu["value"], 1) if cpu and cpu.get("value") else None),
             **extra,
         }
         print(json.dumps(line))

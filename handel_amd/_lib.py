@@ -82,6 +82,13 @@ SIGNATURES = {
     "hg_timing_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
     "hg_timing_read_phase": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
     "hg_sync": (_I, [_P]),
+    "hg_context_bytes": (_SZ, [_P]),
+    "hg_batcher_create": (_I, [_P, _SZ, ctypes.c_uint, ctypes.POINTER(_P)]),
+    "hg_batcher_destroy": (None, [_P]),
+    "hg_batcher_submit": (_I, [_P, _P, _SZ, _P, _P, _P, ctypes.POINTER(_P)]),
+    "hg_batcher_wait": (_I, [_P, _P, _P]),
+    "hg_batcher_verify_aggregate": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
+    "hg_batcher_stats": (_I, [_P, _P, _P]),
 }
 
 

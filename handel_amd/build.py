@@ -19,7 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libhandel_gpu.so")
 DIAG_LIB = os.path.join(OUT_DIR, "libhandel_gpu_diag.so")
-SOURCES = ["bn256_verify.hip", "bn256_pair.hip", "bn256_kernels.hip", "bn256_gt.hip", "hg_api.cpp"]
+SOURCES = ["bn256_verify.hip", "bn256_pair.hip", "bn256_kernels.hip", "bn256_gt.hip", "hg_api.cpp", "hg_batcher.cpp"]
 HEADERS = ["bn256_fp.h", "bn256_curve.h", "bn256_team.h", "bn256_kernels.h", "bn256_constants.h",
            "bn256_g2team.h", "bn256_g2sched.h", "bn256_pairing.h", "bn256_xprog.h", "bn256_xtab.h", "bn256_inv.h", "bn256_agg.h", "bn256_gt.h"]
 ARCH = os.environ.get("HG_OFFLOAD_ARCH", "gfx950")
@@ -88,7 +88,28 @@ def build_native_tests(verbose: bool = True) -> str:
     return ABI_THREADS
 
 
+HANDEL_PROXY = os.path.join(OUT_DIR, "handel_proxy")
+
+
+def build_proxy(verbose: bool = True) -> str:
+    """tests/native/handel_proxy.c: the config-4 process-model proxy (forks
+    the processes first, each dlopen()s the library: never linked here)."""
+    src = os.path.join(HERE, "..", "tests", "native", "handel_proxy.c")
+    hdr = os.path.join(HERE, "..", "include", "handel_gpu.h")
+    if os.path.exists(HANDEL_PROXY) and os.path.getmtime(HANDEL_PROXY) >= max(os.path.getmtime(src),
+                                                                             os.path.getmtime(hdr)):
+        return HANDEL_PROXY
+    os.makedirs(OUT_DIR, exist_ok=True)
+    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-I", os.path.join(HERE, "..", "include"), src, "-ldl",
+           "-lpthread", "-o", HANDEL_PROXY]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return HANDEL_PROXY
+
+
 if __name__ == "__main__":
     print(build_library(force="--force" in sys.argv, diag="--diag" in sys.argv))
     if "--diag" not in sys.argv:
         print(build_native_tests())
+        print(build_proxy())

@@ -645,9 +645,11 @@ HG_DEV bool t12_equal(const Team& T, int a, int b) {
 }
 
 // FE(Miller(G2Base at -sig)) == Y_r  <=>  e(H, agg) * e(-sig, G2Base) == 1
-template <int TEAMS>
+// kStore: write FE(Miller(G2Base at -sig)) to fe[r] instead (the fold runs
+// beside this kernel on a second stream; k_gt_compare finishes the check)
+template <int TEAMS, bool kStore>
 __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y,
-                                                   int32_t* codes) {
+                                                   Gt* fe, int32_t* codes) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
   Team T = make_team(lds, kTeamWords);
   uint32_t* F = team_regs(T);
@@ -658,10 +660,31 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, int n, c
   XStream S = x_stream();
   team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, final_exp_hint());
   team_final_exp(T, F, S);
+  if (kStore) {
+    team_sync();
+    if (valid) gt_store(T, S_F, fe + idx);
+    return;
+  }
   gt_load(T, S_A, y + ci);
   team_sync();
   const bool ok = t12_equal(T, S_F, S_A);
   if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
+}
+
+// fe[r] == y[r] (both canonical: word equality) for every request still HG_OK;
+// one wave per request, lane l < 60 compares words 2l, 2l + 1
+__global__ __launch_bounds__(64) void k_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes) {
+  const int r = blockIdx.x;
+  if (r >= n) return;
+  const int l = threadIdx.x;
+  bool eq = true;
+  if (l < 60) {
+    const uint2 a = reinterpret_cast<const uint2*>(fe[r].w)[l];
+    const uint2 b = reinterpret_cast<const uint2*>(y[r].w)[l];
+    eq = a.x == b.x && a.y == b.y;
+  }
+  const bool all = __ballot(!eq) == 0;
+  if (l == 0 && codes[r] == HG_OK) codes[r] = all ? HG_OK : HG_ERR_SIG_INVALID;
 }
 
 // ------------------------------------------------------------------ launchers
@@ -693,7 +716,13 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
   k_gt_combine<<<n, 64, 0, s>>>(n, w.hdr, w.multi, w.plan, w.partial, y);
 }
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
-  if (n > 0) k_verify_sig<4><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, y, codes);
+  if (n > 0) k_verify_sig<4, false><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, y, nullptr, codes);
+}
+void launch_sig_pairing(const PointG1* sigs, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
+  if (n > 0) k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, nullptr, fe, nullptr);
+}
+void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s) {
+  if (n > 0) k_gt_compare<<<n, 64, 0, s>>>(fe, y, n, codes);
 }
 
 }  // namespace hg

@@ -202,6 +202,11 @@ struct hg_ctx {
   DevBuf<int2> gt_ord;
   DevBuf<int> gt_multi;
   DevBuf<Gt> gt_partial, gt_y;
+  // the fold runs on a side stream beside the pairing kernel (GT path): the
+  // FE values of the batch land in gt_fe, k_gt_compare joins the two
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  DevBuf<Gt> gt_fe;
   // submission order across streams: the event recorded after the last
   // submission and the stream it ran on (the workspaces above are shared)
   hipEvent_t last_ev = nullptr;
@@ -331,7 +336,13 @@ static void release_all(hg_ctx* c) {
   c->gt_multi.release();
   c->gt_partial.release();
   c->gt_y.release();
+  c->gt_fe.release();
   c->gt_level = 0;
+  if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  c->side = nullptr;
+  c->ev_fork = c->ev_join = nullptr;
   for (auto& ph : c->events) {
     for (auto& pr : ph) {
       (void)hipEventDestroy(pr.first);
@@ -641,6 +652,21 @@ static int gt_acquire(hg_ctx* c, hipStream_t s, size_t n, const FoldCaps& caps, 
   return HG_OK;
 }
 
+// The fold beside the pairing kernel (default; HG_GT_OVERLAP=0 runs them one
+// after the other, with the comparison inside k_verify_sig): k_verify_sig at
+// one wave per SIMD leaves issue slots and LDS for the fold's waves.
+static bool gt_overlap() {
+  static const bool on = env_int("HG_GT_OVERLAP", 1, 0, 1) != 0;
+  return on;
+}
+static hipError_t ensure_side(hg_ctx* c) {
+  hipError_t e = hipSuccess;
+  if (!c->side) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess && !c->ev_fork) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess && !c->ev_join) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+  return e;
+}
+
 // the level check of processing.go:350-352 on the device
 __global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -689,8 +715,34 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   if (use_gt && !g2_fold) {
     // GT path, verdicts only: level check, signature decode and the fold's
     // counters in one launch, then the fold and the check on d_codes
+    const bool overlap = gt_overlap();
+    if (overlap) {
+      HG_CHECK(c, ensure_side(c));
+      HG_CHECK(c, c->gt_fe.ensure(n));
+    }
     launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, c->pts1.p, d_codes, (int*)gw.hdr,
                         (int)(sizeof(GtHdr) / sizeof(int)), s);
+    if (overlap) {
+      // s: prologue -> pairing ............ -> wait -> compare
+      // side:          wait -> plan, chunks, combine -> join
+      HG_CHECK(c, hipEventRecord(c->ev_fork, s));
+      PhaseTimer t(c, HG_PHASE_VERIFY, s);
+      launch_sig_pairing(c->pts1.p, (int)n, c->d_lines, c->gt_fe.p, s);
+      t.stop();
+      HG_CHECK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      PhaseTimer fold(c, HG_PHASE_AGGREGATE, c->side);
+      launch_gt_fold(d_reqs, (int)n, d_words, d_codes, (int)c->nreg, c->block_levels,
+                     level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, false, c->side);
+      fold.stop();
+      HG_CHECK(c, hipEventRecord(c->ev_join, c->side));
+      HG_CHECK(c, hipStreamWaitEvent(s, c->ev_join, 0));
+      launch_gt_compare(c->gt_fe.p, c->gt_y.p, (int)n, d_codes, s);
+      all.stop();
+      int rc = check_launch(c);
+      if (rc) return rc;
+      HG_CHECK(c, sub.finish());
+      return HG_OK;
+    }
     PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
     launch_gt_fold(d_reqs, (int)n, d_words, d_codes, (int)c->nreg, c->block_levels,
                    level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, false, s);
@@ -878,6 +930,7 @@ void hg_destroy(hg_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->last_ev) (void)hipEventSynchronize(c->last_ev);  // a submission on a caller stream
   release_all(c);
   delete c;
@@ -1298,6 +1351,21 @@ int hg_diag_read(hg_ctx* c, uint64_t* out, size_t n) {
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   if (c->last_ev) HG_CHECK(c, hipEventSynchronize(c->last_ev));
   return diag_read(out, n) == 0 ? HG_OK : HG_ERR_ARG;
+}
+
+size_t hg_context_bytes(hg_ctx* c) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  size_t b = sizeof(LineCoef) * kNumLines + sizeof(PointG1) + 32;
+  b += c->reg.cap * sizeof(PointG2) + c->blocks.cap * sizeof(PointG2) + c->wsum.cap * sizeof(PointG2);
+  b += c->bytes_a.cap + c->bytes_b.cap + c->pts2.cap * sizeof(PointG2) + c->pts1.cap * sizeof(PointG1);
+  b += c->pts1b.cap * sizeof(PointG1) + c->checks.cap * sizeof(CheckIn);
+  b += (c->codes_a.cap + c->codes_b.cap + c->codes_c.cap) * sizeof(int32_t) + c->reqs.cap * sizeof(hg_request);
+  b += c->order.cap * sizeof(int) + c->agg_ws.cap + c->words.cap * sizeof(uint64_t);
+  b += (c->gt_key.cap + c->gt_w8.cap + c->gt_win.cap + c->gt_blk.cap + c->gt_partial.cap + c->gt_y.cap) * sizeof(Gt);
+  b += c->gt_plan.cap * sizeof(GtReq) + c->gt_hdr.cap * sizeof(GtHdr) + c->gt_terms.cap * sizeof(uint32_t);
+  b += c->gt_ord.cap * sizeof(int2) + c->gt_multi.cap * sizeof(int) + c->gt_fe.cap * sizeof(Gt);
+  return b;
 }
 
 int hg_timing_enable(hg_ctx* c, int on) {

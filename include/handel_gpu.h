@@ -239,6 +239,40 @@ int hg_diag_read(hg_ctx* ctx, uint64_t* out, size_t n);
 /* Wait for all work submitted on the context's stream. */
 int hg_sync(hg_ctx* ctx);
 
+/* Device memory held by the context (registry, its sums, GT tables,
+ * workspaces), in bytes: the HBM one simul process's verifier costs. */
+size_t hg_context_bytes(hg_ctx* ctx);
+
+/* ---------------------------------------------------------------- batcher
+ * A launch-merging request queue on one context, for callers that verify one
+ * multisignature at a time: each Handel instance's processLoop checks one
+ * signature per step (processing.go:228-287 -> verifySignature :342-368) and
+ * a simul process runs k instances concurrently (simul/node/main.go:63-131).
+ * A dispatcher thread merges the queued requests into one
+ * hg_verify_aggregate_msg batch (grouped by message, at most max_batch; an
+ * idle dispatcher waits at most max_wait_us after the oldest request for
+ * more) and hands every caller its own code. Verdicts are a pure function of
+ * (msg, range, bitset, sig), so batching cannot change them. The context must
+ * outlive the batcher. */
+typedef struct hg_batcher hg_batcher;
+typedef struct hg_ticket hg_ticket;
+int hg_batcher_create(hg_ctx* ctx, size_t max_batch, unsigned max_wait_us, hg_batcher** out);
+/* Verifies what is still queued, then stops the dispatcher. */
+void hg_batcher_destroy(hg_batcher* b);
+/* Queues one request: req->offset / bitlen / level_size as in hg_request
+ * (word_offset ignored), its ceil(bitlen/64) bitset words at `words`, the
+ * 64-byte signature. Inputs are copied; the ticket is released by
+ * hg_batcher_wait, exactly once. */
+int hg_batcher_submit(hg_batcher* b, const uint8_t* msg, size_t len, const hg_request* req, const uint64_t* words,
+                      const uint8_t* sig, hg_ticket** out);
+/* Blocks until the ticket's batch ran; *code = its hg_code. Returns HG_OK, or
+ * the batch's HG_ERR_ARG / HG_ERR_DEVICE. */
+int hg_batcher_wait(hg_batcher* b, hg_ticket* t, int32_t* code);
+/* hg_batcher_submit + hg_batcher_wait: one processing.go verifySignature. */
+int hg_batcher_verify_aggregate(hg_batcher* b, const uint8_t* msg, size_t len, const hg_request* req,
+                                const uint64_t* words, const uint8_t* sig, int32_t* code);
+int hg_batcher_stats(hg_batcher* b, uint64_t* batches, uint64_t* requests);
+
 #ifdef __cplusplus
 }
 #endif
