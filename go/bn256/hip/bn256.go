@@ -123,10 +123,18 @@ type PublicKey struct {
 	aggErr  error
 }
 
+// bindRegistry annotates a key with its index in r (the latest load that
+// holds it wins). Index-based use checks that the binding is usable: same
+// engine, and r still the registry loaded on it (see indexed).
 func (p *PublicKey) bindRegistry(r *Registry, i int) {
 	p.reg = r
 	p.idx = i
 }
+
+// indexed reports whether index-based requests for this key or aggregate are
+// valid now: its registry is the one loaded on the key's own engine. The
+// caller holds p.e.regMu for reading until its request has run.
+func (p *PublicKey) indexed() bool { return p.reg != nil && p.reg.e == p.e && p.reg.current() }
 
 func (p *PublicKey) isEmpty() bool { return p.p == nil && p.bits == nil }
 
@@ -154,6 +162,13 @@ func (p *PublicKey) point() ([]byte, error) {
 		return p.p, nil
 	}
 	p.aggOnce.Do(func() {
+		p.e.regMu.RLock()
+		defer p.e.regMu.RUnlock()
+		if !p.indexed() {
+			// the registry was replaced (or belongs to another engine): fold its points
+			p.agg, p.aggErr = p.reg.foldPoints(p.e, p.bits)
+			return
+		}
 		n := p.reg.size
 		out, codes, err := p.e.AggregateKeys([]Request{{Offset: 0, LevelSize: n, BitLen: n, Words: p.bits}})
 		if err == nil {
@@ -222,8 +237,8 @@ func (p *PublicKey) Combine(pp handel.PublicKey) handel.PublicKey {
 		return pp
 	}
 	p2 := pp.(*PublicKey)
-	if a, ra, ok := p.registryBits(); ok {
-		if b, rb, ok2 := p2.registryBits(); ok2 && ra == rb {
+	if a, ra, ok := p.registryBits(); ok && ra.e == p.e {
+		if b, rb, ok2 := p2.registryBits(); ok2 && ra == rb && p2.e == p.e {
 			w := make([]uint64, len(a))
 			disjoint := true
 			for i := range a {
@@ -275,16 +290,27 @@ func (p *PublicKey) VerifySignature(msg []byte, sig handel.Signature) error {
 	if err != nil {
 		return err
 	}
-	if p.lazy() {
-		n := p.reg.size
-		return p.e.submit(msg, &Request{Offset: 0, LevelSize: n, BitLen: n, Words: p.bits, Sig: s}, nil)
+	if p.lazy() || (p.reg != nil && p.idx >= 0) {
+		// index-based requests only while the key's registry is the one loaded
+		// on its engine (held for reading until the request has run)
+		p.e.regMu.RLock()
+		if p.indexed() {
+			defer p.e.regMu.RUnlock()
+			if p.lazy() {
+				n := p.reg.size
+				return p.e.submit(msg, &Request{Offset: 0, LevelSize: n, BitLen: n, Words: p.bits, Sig: s}, nil)
+			}
+			// a registry key (the p2p aggregator's verifyPacket, simul/p2p/aggregator.go:244):
+			// a one-key aggregate request, so the check uses the precomputed e(H, pk)
+			return p.e.submit(msg, &Request{Offset: p.idx, LevelSize: 1, BitLen: 1, Words: []uint64{1}, Sig: s}, nil)
+		}
+		p.e.regMu.RUnlock()
 	}
-	if p.reg != nil && p.idx >= 0 {
-		// a registry key (the p2p aggregator's verifyPacket, simul/p2p/aggregator.go:244):
-		// a one-key aggregate request, so the check uses the precomputed e(H, pk)
-		return p.e.submit(msg, &Request{Offset: p.idx, LevelSize: 1, BitLen: 1, Words: []uint64{1}, Sig: s}, nil)
+	pt, err := p.point() // the point path: a key outside the loaded registry, or a stale aggregate
+	if err != nil {
+		return err
 	}
-	return p.e.submit(msg, nil, &single{pk: p.p, sig: s})
+	return p.e.submit(msg, nil, &single{pk: pt, sig: s})
 }
 
 // SecretKey is the secret scalar (bn256/go/bn256.go:122-166).

@@ -10,12 +10,120 @@ import (
 	"crypto/rand"
 	"sync"
 	"testing"
+	"time"
 
 	h "github.com/ConsenSys/handel"
 	"github.com/stretchr/testify/require"
 )
 
 var funky = []byte("Get Funky Tonight")
+
+// TestHandel is the reference's in-protocol test (bn256/go/bn256_test.go:13-37):
+// 37 Handel instances with real BLS reach the full multisignature. Here the
+// keys are hip keys, loaded as the engine's registry before the run, so every
+// Combine Handel does over registry keys stays a bitset and every
+// verifySignature (processing.go:342-368) becomes one aggregate request of the
+// engine's batcher; the GT tables are prepared for the message.
+func TestHandel(t *testing.T) {
+	n := 37
+	config := h.DefaultConfig(n)
+	msg := []byte("Peaches and Cream")
+	e, err := NewEngine(0, FlavorGo)
+	require.NoError(t, err)
+	defer e.Close()
+	cons := NewConstructorOn(e)
+	secretKeys := make([]h.SecretKey, n)
+	pubKeys := make([]h.PublicKey, n)
+	ids := make([]h.Identity, n)
+	for i := 0; i < n; i++ {
+		sec, pub := cons.KeyPair(rand.Reader)
+		secretKeys[i] = sec
+		pubKeys[i] = pub
+		// the identities NewTest builds (test.go:35-47): same ids, same key objects
+		ids[i] = h.NewStaticIdentity(int32(i), "", pub)
+	}
+	_, err = e.LoadRegistry(h.NewArrayRegistry(ids))
+	require.NoError(t, err)
+	require.NoError(t, e.PrepareAggregate(msg))
+	test := h.NewTest(secretKeys, pubKeys, cons, msg, config)
+	test.Start()
+	defer test.Stop()
+
+	select {
+	case <-test.WaitCompleteSuccess():
+	case <-time.After(100 * time.Second):
+		t.FailNow()
+	}
+}
+
+// A registry replaced on its engine: keys and lazy aggregates bound to the old
+// one must not be checked by index against the new one (they take the point
+// path), and the old Registry's batched entry points refuse to run.
+func TestRegistryReplaced(t *testing.T) {
+	e, err := NewEngine(0, FlavorGo)
+	require.NoError(t, err)
+	defer e.Close()
+	regA, sksA, rA := testRegistry(t, e, 16)
+	_, _, rB := testRegistry(t, e, 16) // replaces A on the engine
+	require.False(t, rA.current())
+	require.True(t, rB.current())
+	id3, _ := regA.Identity(3)
+	id5, _ := regA.Identity(5)
+	s3, _ := sksA[3].Sign(funky, nil)
+	s5, _ := sksA[5].Sign(funky, nil)
+	require.NoError(t, id3.PublicKey().VerifySignature(funky, s3))
+	agg := id3.PublicKey().Combine(id5.PublicKey())
+	require.True(t, agg.(*PublicKey).lazy())
+	require.NoError(t, agg.VerifySignature(funky, s3.Combine(s5)))
+	require.EqualError(t, id3.PublicKey().VerifySignature(funky, s5), "bn256: signature invalid")
+	bs := h.NewWilffBitset(16)
+	bs.Set(3, true)
+	errs := rA.VerifyMultiSignatures(funky, []*h.MultiSignature{{BitSet: bs, Signature: s3}})
+	require.EqualError(t, errs[0], "hip: registry is no longer loaded on its engine")
+}
+
+// A key bound to a registry of another engine is checked by its point.
+func TestKeyOfOtherEngine(t *testing.T) {
+	a, err := NewEngine(0, FlavorGo)
+	require.NoError(t, err)
+	defer a.Close()
+	b, err := NewEngine(0, FlavorGo)
+	require.NoError(t, err)
+	defer b.Close()
+	regA, sksA, _ := testRegistry(t, a, 8)
+	id2, _ := regA.Identity(2)
+	// the same key objects loaded on engine b: bound to b's registry now
+	ids := make([]h.Identity, 8)
+	for i := range ids {
+		ids[i], _ = regA.Identity(i)
+	}
+	_, err = b.LoadRegistry(h.NewArrayRegistry(ids))
+	require.NoError(t, err)
+	s2, _ := sksA[2].Sign(funky, nil)
+	require.NoError(t, id2.PublicKey().VerifySignature(funky, s2)) // key of engine a, registry of b: point path
+}
+
+// Range checks every identity of a level slice.
+func TestRegistryRangeContiguous(t *testing.T) {
+	e, err := NewEngine(0, FlavorGo)
+	require.NoError(t, err)
+	defer e.Close()
+	reg, _, r := testRegistry(t, e, 16)
+	slice := func(ix ...int) []h.Identity {
+		out := make([]h.Identity, len(ix))
+		for j, i := range ix {
+			out[j], _ = reg.Identity(i)
+		}
+		return out
+	}
+	off, err := r.Range(slice(4, 5, 6, 7))
+	require.NoError(t, err)
+	require.Equal(t, 4, off)
+	_, err = r.Range(slice(4, 9, 6, 7)) // right endpoints, wrong middle
+	require.Error(t, err)
+	_, err = r.Range(slice(14, 15, 16))
+	require.Error(t, err)
+}
 
 func TestSign(t *testing.T) {
 	sk, pk, err := NewKeyPair(rand.Reader)

@@ -178,10 +178,10 @@ func (e *Engine) SetMessage(msg []byte) error {
 // Without it the engine builds the tables by request volume (see
 // AggregateTables).
 func (e *Engine) PrepareAggregate(msg []byte) error {
-	if err := e.SetMessage(msg); err != nil {
-		return err
-	}
-	switch rc := C.hg_prepare_aggregate(e.ctx); rc {
+	// hashing and the build under one lock hold of the context
+	// (hg_prepare_aggregate_msg): a concurrent caller with another message
+	// cannot take the tables in between
+	switch rc := C.hg_prepare_aggregate_msg(e.ctx, bytePtr(msg), C.size_t(len(msg))); rc {
 	case C.HG_OK:
 		return nil
 	case C.HG_ERR_HASH_EOF:
@@ -198,6 +198,33 @@ func (e *Engine) PrepareAggregate(msg []byte) error {
 func (e *Engine) AggregateTables() int {
 	return int(C.hg_aggregate_tables(e.ctx))
 }
+
+// SetAggregateLevel pins the table level of aggregate checks (0..2) or, with
+// -1, returns them to the volume policy (hg_set_aggregate_level).
+func (e *Engine) SetAggregateLevel(level int) error {
+	if rc := C.hg_set_aggregate_level(e.ctx, C.int(level)); rc != C.HG_OK {
+		return e.fail(rc)
+	}
+	return nil
+}
+
+// SetTableBudget bounds the HBM of this engine's aggregate tables: processes
+// sharing one GPU (simul's P processes x k instances) each take a share. A
+// level that does not fit is skipped (hg_set_table_budget).
+func (e *Engine) SetTableBudget(bytes uint64) error {
+	if rc := C.hg_set_table_budget(e.ctx, C.size_t(bytes)); rc != C.HG_OK {
+		return e.fail(rc)
+	}
+	return nil
+}
+
+// RegistryNonG2 is the number of loaded registry keys on the twist but
+// outside G2 (accepted by x/crypto's Unmarshal); such a registry is checked
+// with the G2 point fold and two pairings (hg_registry_non_g2).
+func (e *Engine) RegistryNonG2() int { return int(C.hg_registry_non_g2(e.ctx)) }
+
+// DeviceBytes is the device memory the context holds (hg_context_bytes).
+func (e *Engine) DeviceBytes() uint64 { return uint64(C.hg_context_bytes(e.ctx)) }
 
 // VerifyBatch runs n = len(sigs)/64 independent PublicKey.VerifySignature(msg,
 // sig) checks (bn256/go/bn256.go:82-94) in one launch; pks holds n 128-byte

@@ -17,6 +17,7 @@ type Registry struct {
 	e     *Engine
 	size  int
 	index map[int32]int // identity ID -> registry index
+	keys  [][]byte      // the key marshals, for folds once this registry is no longer loaded
 }
 
 // LoadRegistry uploads reg to the engine. Every identity's PublicKey must be
@@ -44,32 +45,89 @@ func (e *Engine) LoadRegistry(reg handel.Registry) (*Registry, error) {
 		keys[i] = pk
 		index[id.ID()] = i
 	}
+	// the load replaces the context's registry: no index-based check may run
+	// against it meanwhile (they hold regMu for reading, see current)
+	e.regMu.Lock()
+	defer e.regMu.Unlock()
+	e.reg = nil
 	if _, err := e.loadRegistry(buf); err != nil {
 		return nil, err
 	}
-	r := &Registry{e: e, size: n, index: index}
+	marshals := make([][]byte, n)
+	for i := range marshals {
+		marshals[i] = buf[128*i : 128*i+128]
+	}
+	r := &Registry{e: e, size: n, index: index, keys: marshals}
 	for i, pk := range keys {
 		pk.bindRegistry(r, i)
 	}
-	e.regMu.Lock()
 	e.reg = r
-	e.regMu.Unlock()
 	return r, nil
+}
+
+// current reports whether r is the registry its engine's context holds now,
+// so index-based requests against the context mean r's keys. The caller must
+// hold r.e.regMu (for reading) until its request has run.
+func (r *Registry) current() bool { return r != nil && r.e.reg == r }
+
+// foldPoints sums the keys whose bits are set with point additions (batched
+// PublicKey.Combine, pairwise tree), for a lazy aggregate whose registry is no
+// longer the loaded one.
+func (r *Registry) foldPoints(e *Engine, bits []uint64) ([]byte, error) {
+	var pts [][]byte
+	for i := 0; i < r.size; i++ {
+		if bits[i>>6]>>uint(i&63)&1 == 1 {
+			pts = append(pts, r.keys[i])
+		}
+	}
+	if len(pts) == 0 {
+		return nil, e.CodeError(codeEmptyAgg)
+	}
+	for len(pts) > 1 {
+		half := len(pts) / 2
+		a := make([]byte, 0, 128*half)
+		b := make([]byte, 0, 128*half)
+		for i := 0; i < half; i++ {
+			a = append(a, pts[2*i]...)
+			b = append(b, pts[2*i+1]...)
+		}
+		out, codes, err := e.CombineG2(a, b)
+		if err != nil {
+			return nil, err
+		}
+		next := make([][]byte, 0, half+1)
+		for i := 0; i < half; i++ {
+			if err := e.CodeError(codes[i]); err != nil {
+				return nil, err
+			}
+			next = append(next, out[128*i:128*i+128])
+		}
+		if len(pts)%2 == 1 {
+			next = append(next, pts[len(pts)-1])
+		}
+		pts = next
+	}
+	return pts[0], nil
 }
 
 // Size is the number of registry keys.
 func (r *Registry) Size() int { return r.size }
 
 // Range maps a level's identities (Partitioner.IdentitiesAt, a contiguous
-// registry slice by partitioner.go:133-178) to its registry offset.
+// registry slice by partitioner.go:133-178) to its registry offset. Every
+// identity is checked: identity j must sit at registry index offset + j.
 func (r *Registry) Range(ids []handel.Identity) (offset int, err error) {
 	if len(ids) == 0 {
 		return 0, nil
 	}
 	lo, ok := r.index[ids[0].ID()]
-	hi, ok2 := r.index[ids[len(ids)-1].ID()]
-	if !ok || !ok2 || hi-lo != len(ids)-1 {
+	if !ok || lo+len(ids) > r.size {
 		return 0, errors.New("hip: level identities are not a contiguous registry range")
+	}
+	for j, id := range ids {
+		if k, ok := r.index[id.ID()]; !ok || k != lo+j {
+			return 0, errors.New("hip: level identities are not a contiguous registry range")
+		}
 	}
 	return lo, nil
 }
@@ -95,6 +153,16 @@ func bitsetWords(bs handel.BitSet) []uint64 {
 // whole fails, every request gets that error: nothing is reported valid.
 func (r *Registry) VerifyBatch(msg []byte, reqs []handel.BatchRequest) []error {
 	out := make([]error, len(reqs))
+	r.e.regMu.RLock()
+	defer r.e.regMu.RUnlock()
+	if !r.current() {
+		// the engine has loaded another registry since: index-based requests
+		// would check against its keys
+		for i := range out {
+			out[i] = errors.New("hip: registry is no longer loaded on its engine")
+		}
+		return out
+	}
 	creqs := make([]Request, 0, len(reqs))
 	where := make([]int, 0, len(reqs))
 	for i, q := range reqs {
@@ -138,6 +206,14 @@ func (r *Registry) VerifyBatch(msg []byte, reqs []handel.BatchRequest) []error {
 // VerifySignature error.
 func (r *Registry) VerifyMultiSignatures(msg []byte, ms []*handel.MultiSignature) []error {
 	out := make([]error, len(ms))
+	r.e.regMu.RLock()
+	defer r.e.regMu.RUnlock()
+	if !r.current() {
+		for i := range out {
+			out[i] = errors.New("hip: registry is no longer loaded on its engine")
+		}
+		return out
+	}
 	lens := make([]int, 0, len(ms))
 	words := make([][]uint64, 0, len(ms))
 	sigs := make([]byte, 0, 64*len(ms))
