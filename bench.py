@@ -538,6 +538,11 @@ def main():
         want = [pack_verdicts(torch.from_numpy(head.expect))]
         assert torch.equal(gathered[rank].cpu(), want[0]), "gathered bitset of this rank differs"
     ph = timed_phases(eng, lambda: [head.submit() for _ in range(5)])
+    # the kernels on their own (fold, then the pairing kernel: no overlap),
+    # for the per-kernel rooflines
+    eng.set_fold_overlap(False)
+    ph_seq = timed_phases(eng, lambda: [head.submit() for _ in range(5)])
+    eng.set_fold_overlap(True)
     value = n * args.steps * world / dt
     # the dominant kernels of the step: the GT fold (plan, chunks, combine) and
     # the pairing check, on the work they implement (the primary roofline)
@@ -561,12 +566,15 @@ def main():
                          f"(G2 addition) + {FPMUL_PER_CHECK} (two-pairing check), x {MADS_PER_FPMUL} u32 mads; mean "
                          f"{head.signers.mean():.1f} set bits",
                  "note": "work the GT path does not run is credited here; not a fraction of any peak"}
-    roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph["verify"], "k_verify_sig", r"k_verify_sig",
+    roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph_seq["verify"], "k_verify_sig", r"k_verify_sig",
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
-                           "+ final exponentiation, oracle op count)")
-    roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
+                           "+ final exponentiation, oracle op count); kernel alone (fold not beside it)")
+    roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph_seq["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
                          r"k_gt_(plan|chunks|combine)",
-                         f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each)")
+                         f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each); "
+                         "kernels alone (not beside the pairing kernel)")
+    roof["kernels_alone_ms"] = {"fold": round(ph_seq["fold"], 4), "k_verify": round(ph_seq["verify"], 4),
+                                "submit": round(ph_seq["submit"], 4)}
 
     extra = {}
     if not args.no_extra:
@@ -646,6 +654,11 @@ def main():
             # a verifier serving a continuous stream: batches in flight on several
             # HIP streams, one engine context (own workspaces) per stream
             engs = [eng] + [Engine(device=local_dev, flavor="go") for _ in range(args.pipeline - 1)]
+            # with several batches in flight, each batch's fold runs before its
+            # pairing kernel: the other batch's kernels fill the gaps
+            # (profiles/r03h_pipeline_ab.json: 4.36 vs 4.23 M/s for two batches)
+            for e in engs:
+                e.set_fold_overlap(False)
             for e in engs[1:]:
                 assert e.set_message(LIB_MESSAGE) == 0
                 assert not e.registry_load(head.reg).any()
@@ -664,6 +677,7 @@ def main():
                                   "unit": "verifications/s", "batches_in_flight": len(engs), "batch": n,
                                   "ms_per_step": round(pdt / args.steps * 1e3, 4),
                                   "note": "headline batch on each of the streams; throughput with batches overlapped"}
+            eng.set_fold_overlap(True)
             for e in engs[1:]:
                 e.close()
 

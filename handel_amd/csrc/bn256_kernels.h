@@ -34,8 +34,8 @@ using AggRequest = hg_request;
 
 void launch_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int32_t* codes, hipStream_t s);
 void launch_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes, hipStream_t s);
-// flag[i] = 1 iff the decoded key reg[i] is on the twist but outside G2 (n * P != inf)
-void launch_g2_subgroup(const PointG2* reg, int n, int32_t* flag, hipStream_t s);
+// *count += the decoded keys reg[i] on the twist but outside G2 (n * P != inf)
+void launch_g2_subgroup(const PointG2* reg, int n, int* count, hipStream_t s);
 void launch_encode_g2(const PointG2* in, int n, uint8_t* out, hipStream_t s);
 void launch_encode_g1(const PointG1* in, int n, uint8_t* out, hipStream_t s);
 void launch_g2_mul_base(const uint8_t* scalars, int n, PointG2* out, hipStream_t s);

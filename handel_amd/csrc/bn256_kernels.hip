@@ -81,16 +81,15 @@ __global__ __launch_bounds__(64) void k_decode_g2(const uint8_t* bytes, int n, i
   codes[i] = code;
 }
 
-// G2 membership of decoded registry keys: flag[i] = 1 iff n * key_i != inf
-// (key_i on the twist but outside the order-n subgroup G2). x/crypto's
+// G2 membership of decoded registry keys: *count += 1 for every key with
+// n * key != inf (on the twist but outside the order-n subgroup G2). x/crypto's
 // G2.Unmarshal (bn256/go/bn256.go:113-120) accepts such keys; the GT path's
 // bilinearity argument only holds on G2, so a registry holding one is served
 // by the G2 fold + two-pairing check instead (hg_api.cpp gt_max_level).
-__global__ __launch_bounds__(64) void k_g2_subgroup(const PointG2* reg, int n, int32_t* flag) {
+__global__ __launch_bounds__(64) void k_g2_subgroup(const PointG2* reg, int n, int* count) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const PointG2 P = reg[i];
-  int32_t out = 0;
   if (!P.inf) {
     const uint32_t order[8] = {HG_ORDER32};
     G2J a, r;
@@ -98,9 +97,8 @@ __global__ __launch_bounds__(64) void k_g2_subgroup(const PointG2* reg, int n, i
     a.y = P.y;
     f2_one(a.z);
     g2_mul(r, a, order);
-    out = g2_is_inf(r) ? 0 : 1;
+    if (!g2_is_inf(r)) atomicAdd(count, 1);
   }
-  flag[i] = out;
 }
 
 __global__ __launch_bounds__(64) void k_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes) {
@@ -799,8 +797,8 @@ static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 void launch_decode_g2(const uint8_t* bytes, int n, int flavor, PointG2* out, int32_t* codes, hipStream_t s) {
   if (n > 0) k_decode_g2<<<nblk(n, 64), 64, 0, s>>>(bytes, n, flavor, out, codes);
 }
-void launch_g2_subgroup(const PointG2* reg, int n, int32_t* flag, hipStream_t s) {
-  if (n > 0) k_g2_subgroup<<<(n + 63) / 64, 64, 0, s>>>(reg, n, flag);
+void launch_g2_subgroup(const PointG2* reg, int n, int* count, hipStream_t s) {
+  if (n > 0) k_g2_subgroup<<<(n + 63) / 64, 64, 0, s>>>(reg, n, count);
 }
 void launch_decode_g1(const uint8_t* bytes, int n, int flavor, PointG1* out, int32_t* codes, hipStream_t s) {
   if (n > 0) k_decode_g1<<<nblk(n, 64), 64, 0, s>>>(bytes, n, flavor, out, codes);

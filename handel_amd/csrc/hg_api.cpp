@@ -191,8 +191,13 @@ struct hg_ctx {
   int gt_cap = 2;
   size_t table_budget = SIZE_MAX;  // bytes of GT tables (hg_set_table_budget)
   // registry keys on the twist but outside G2 (go flavor only: x/crypto's
-  // Unmarshal accepts them); any such key pins the registry to level 0
+  // Unmarshal accepts them); any such key pins the registry to level 0. The
+  // check (one n*Q per key, ~7 ms of single-lane latency) runs on the side
+  // stream after the load; it is waited for only when a GT level is wanted.
   size_t reg_non_g2 = 0;
+  bool sub_pending = false;
+  hipEvent_t ev_sub = nullptr;
+  DevBuf<int> sub_count;
   DevBuf<Gt> gt_key, gt_w8, gt_win, gt_blk;  // gt_w8: 8-key windows, gt_win: 16-key windows
   GtBlockIndex gt_bi{};
   // GT fold workspaces
@@ -207,6 +212,7 @@ struct hg_ctx {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   DevBuf<Gt> gt_fe;
+  bool overlap = true;  // hg_set_fold_overlap; HG_GT_OVERLAP=0 gives new contexts false
   // submission order across streams: the event recorded after the last
   // submission and the stream it ran on (the workspaces above are shared)
   hipEvent_t last_ev = nullptr;
@@ -341,8 +347,11 @@ static void release_all(hg_ctx* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->ev_sub) (void)hipEventDestroy(c->ev_sub);
+  c->sub_count.release();
+  c->sub_pending = false;
   c->side = nullptr;
-  c->ev_fork = c->ev_join = nullptr;
+  c->ev_fork = c->ev_join = c->ev_sub = nullptr;
   for (auto& ph : c->events) {
     for (auto& pr : ph) {
       (void)hipEventDestroy(pr.first);
@@ -471,8 +480,19 @@ static int gt_forced_level() {
   }();
   return lvl;
 }
+// the registry's G2 membership count, waiting for its check if still running
+static int resolve_subgroup(hg_ctx* c) {
+  if (!c->sub_pending) return HG_OK;
+  int cnt = 0;
+  HG_CHECK(c, hipEventSynchronize(c->ev_sub));
+  HG_CHECK(c, hipMemcpy(&cnt, c->sub_count.p, sizeof cnt, hipMemcpyDeviceToHost));
+  c->reg_non_g2 = (size_t)cnt;
+  c->sub_pending = false;
+  return HG_OK;
+}
+// the highest table level the registry may use (the membership check must be resolved)
 static int gt_max_level(const hg_ctx* c) {
-  if (c->reg_non_g2) return 0;
+  if (c->reg_non_g2 || c->sub_pending) return 0;
   const int top = c->nreg <= kGtMaxRegistry ? 2 : 1;
   return top < c->gt_cap ? top : c->gt_cap;
 }
@@ -565,6 +585,9 @@ static void gt_lower_cap(hg_ctx* c, int cap) {
 // them towards the volume policy)
 static int gt_submission_level(hg_ctx* c, size_t n) {
   if (c->hash_eof || c->nreg == 0) return 0;
+  // a GT level needs the registry's G2 membership (resolved only then)
+  const bool wants_gt = c->pinned_level > 0 || c->gt_level > 0 || c->gt_requests + n >= kGtLevel1Requests;
+  if (wants_gt && resolve_subgroup(c) != HG_OK) return 0;
   const int top = gt_max_level(c);
   if (c->pinned_level >= 0) return c->pinned_level < top ? c->pinned_level : top;
   c->gt_requests += n;
@@ -652,9 +675,10 @@ static int gt_acquire(hg_ctx* c, hipStream_t s, size_t n, const FoldCaps& caps, 
   return HG_OK;
 }
 
-// The fold beside the pairing kernel (default; HG_GT_OVERLAP=0 runs them one
-// after the other, with the comparison inside k_verify_sig): k_verify_sig at
-// one wave per SIMD leaves issue slots and LDS for the fold's waves.
+// The fold beside the pairing kernel (default; hg_set_fold_overlap(ctx, 0) or
+// HG_GT_OVERLAP=0 for new contexts runs them one after the other, with the
+// comparison inside k_verify_sig): k_verify_sig at one wave per SIMD leaves
+// issue slots (and LDS for one fold workgroup per CU) for the fold's waves.
 static bool gt_overlap() {
   static const bool on = env_int("HG_GT_OVERLAP", 1, 0, 1) != 0;
   return on;
@@ -715,7 +739,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
   if (use_gt && !g2_fold) {
     // GT path, verdicts only: level check, signature decode and the fold's
     // counters in one launch, then the fold and the check on d_codes
-    const bool overlap = gt_overlap();
+    const bool overlap = c->overlap;
     if (overlap) {
       HG_CHECK(c, ensure_side(c));
       HG_CHECK(c, c->gt_fe.ensure(n));
@@ -904,6 +928,7 @@ int hg_create(int device, int flavor, hg_ctx** out) {
   c->device = device;
   c->flavor = flavor;
   c->pinned_level = gt_forced_level();
+  c->overlap = gt_overlap();
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->d_lines, sizeof(LineCoef) * kNumLines);
@@ -962,6 +987,9 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   c->gt_level = 0;
   c->gt_requests = 0;
   c->gt_cap = 2;
+  // the previous registry's membership check must be done before its buffer is reused
+  if (c->sub_pending) HG_CHECK(c, hipEventSynchronize(c->ev_sub));
+  c->sub_pending = false;
   c->reg_non_g2 = 0;
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
@@ -984,15 +1012,20 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
     return HG_ERR_PK_UNMARSHAL;
   }
   // go flavor: x/crypto accepts any on-twist key (bn256/go/bn256.go:113-120);
-  // count the keys outside G2 (cf rejected them in the decode above)
-  size_t non_g2 = 0;
+  // count the keys outside G2 on the side stream (cf rejected them in the
+  // decode above); the decode is complete (synchronised above)
+  bool pending = false;
   if (c->flavor == HG_FLAVOR_GO && n) {
-    launch_g2_subgroup(c->reg.p, (int)n, c->codes_a.p, c->stream);
+    HG_CHECK(c, ensure_side(c));
+    if (!c->ev_sub) HG_CHECK(c, hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
+    HG_CHECK(c, c->sub_count.ensure(1));
+    HG_CHECK(c, hipMemsetAsync(c->sub_count.p, 0, sizeof(int), c->side));
+    launch_g2_subgroup(c->reg.p, (int)n, c->sub_count.p, c->side);
     rc = check_launch(c);
     if (rc) return rc;
-    HG_CHECK(c, hipMemcpyAsync(h.data(), c->codes_a.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HG_CHECK(c, hipStreamSynchronize(c->stream));
-    for (size_t i = 0; i < n; i++) non_g2 += h[i] != 0;
+    HG_CHECK(c, hipEventRecord(c->ev_sub, c->side));
+    (void)hipStreamQuery(c->side);  // flush: the check runs now, beside whatever follows
+    pending = true;
   }
   // sums of the aligned power-of-two blocks (Handel's level ranges), level by level
   int K = 0;
@@ -1025,7 +1058,7 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   c->block_levels = K;
   c->nreg = n;
-  c->reg_non_g2 = non_g2;
+  c->sub_pending = pending;
   return HG_OK;
 }
 
@@ -1035,6 +1068,8 @@ static int prepare_aggregate_locked(hg_ctx* c) {
     return HG_ERR_ARG;
   }
   if (c->hash_eof) return HG_ERR_HASH_EOF;
+  int src = resolve_subgroup(c);
+  if (src) return src;
   int level = gt_max_level(c);
   if (c->pinned_level >= 0 && c->pinned_level < level) level = c->pinned_level;
   if (c->gt_level >= level) return HG_OK;
@@ -1077,6 +1112,13 @@ int hg_set_aggregate_level(hg_ctx* c, int level) {
   return HG_OK;
 }
 
+int hg_set_fold_overlap(hg_ctx* c, int on) {
+  if (!c) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->overlap = on != 0;
+  return HG_OK;
+}
+
 int hg_set_table_budget(hg_ctx* c, size_t bytes) {
   if (!c) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1092,6 +1134,7 @@ int hg_set_table_budget(hg_ctx* c, size_t bytes) {
 size_t hg_registry_non_g2(hg_ctx* c) {
   if (!c) return 0;
   std::lock_guard<std::mutex> g(c->mu);
+  if (resolve_subgroup(c) != HG_OK) return 0;
   return c->reg_non_g2;
 }
 
@@ -1365,6 +1408,7 @@ size_t hg_context_bytes(hg_ctx* c) {
   b += (c->gt_key.cap + c->gt_w8.cap + c->gt_win.cap + c->gt_blk.cap + c->gt_partial.cap + c->gt_y.cap) * sizeof(Gt);
   b += c->gt_plan.cap * sizeof(GtReq) + c->gt_hdr.cap * sizeof(GtHdr) + c->gt_terms.cap * sizeof(uint32_t);
   b += c->gt_ord.cap * sizeof(int2) + c->gt_multi.cap * sizeof(int) + c->gt_fe.cap * sizeof(Gt);
+  b += c->sub_count.cap * sizeof(int);
   return b;
 }
 

@@ -101,6 +101,11 @@ class Engine:
         them to the volume policy (-1) (hg_set_aggregate_level)."""
         self._check(self.L.hg_set_aggregate_level(self.ctx, int(level)), "hg_set_aggregate_level")
 
+    def set_fold_overlap(self, on: bool) -> None:
+        """GT fold beside (True) or before (False) the pairing kernel
+        (hg_set_fold_overlap); same verdicts."""
+        self._check(self.L.hg_set_fold_overlap(self.ctx, int(bool(on))), "hg_set_fold_overlap")
+
     def set_table_budget(self, nbytes: int) -> None:
         """Upper bound for this context's GT tables (hg_set_table_budget)."""
         self._check(self.L.hg_set_table_budget(self.ctx, int(nbytes)), "hg_set_table_budget")

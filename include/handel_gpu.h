@@ -167,6 +167,11 @@ int hg_aggregate_tables(hg_ctx* ctx);
  * as above) or, with -1, returns them to the volume policy. New contexts take
  * HG_GT_LEVEL / HG_AGG_PATH=g2 (= 0) from the environment, else -1. */
 int hg_set_aggregate_level(hg_ctx* ctx, int level);
+/* GT path: run the fold on a side stream beside the pairing kernel (1, the
+ * default; HG_GT_OVERLAP=0 makes 0 the default of new contexts) or before it
+ * (0). Same verdicts; the overlap hides the fold when one batch is in flight,
+ * several contexts each with a batch in flight may prefer 0. */
+int hg_set_fold_overlap(hg_ctx* ctx, int on);
 /* Upper bound in bytes for this context's GT tables (default: unlimited, the
  * device's free memory decides). Processes sharing one GPU (simul's P
  * processes x k instances, simul/node/main.go:63-131) give each context a
