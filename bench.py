@@ -174,8 +174,12 @@ def gt_fold_terms(reqs, words, n_reg: int) -> int:
 
 def pmc_traffic(pattern: str):
     """HBM bytes per launch of the kernels matching `pattern`, summed, from the
-    newest committed PMC summary (profiles/*_pmc.csv, tools/rocpd_summary.py):
-    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE."""
+    committed PMC summaries (profiles/*_pmc.csv, tools/rocpd_summary.py):
+    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE per dispatch. Each kernel
+    is taken from the newest summary holding nonzero counters for it (a pass
+    can come back empty for a kernel; the pairing kernels' counters do not
+    depend on the batch's bitsets, so any profile of a 4096-check launch
+    serves)."""
     import csv
     import glob
     import re
@@ -185,15 +189,32 @@ def pmc_traffic(pattern: str):
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.csv")), key=key)
-    for path in reversed(files):
+
+    def read(path):
         vals = {}
         with open(path) as f:
             for row in csv.DictReader(f):
-                if re.search(pattern, row["kernel"]):
-                    vals[row["counter"]] = vals.get(row["counter"], 0.0) + float(row["avg"])
-        if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
-            return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(path, ROOT)
-    return None, None
+                if re.search(pattern, row["kernel"]) and row["counter"] in ("FETCH_SIZE", "WRITE_SIZE"):
+                    vals.setdefault(row["kernel"], {})[row["counter"]] = float(row["avg"])
+        return vals
+
+    tables = [(path, read(path)) for path in reversed(files)]
+    tables = [(p, v) for p, v in tables if v]
+    if not tables:
+        return None, None
+    # the newest summary names the kernels; each one's bytes from the newest
+    # summary with nonzero counters for that kernel
+    got, srcs = {}, set()
+    for name in tables[0][1]:
+        for path, vals in tables:
+            v = vals.get(name, {})
+            if v.get("FETCH_SIZE", 0) > 0 and "WRITE_SIZE" in v:
+                got[name] = int((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024)
+                srcs.add(os.path.relpath(path, ROOT))
+                break
+    if not got:
+        return None, None
+    return sum(got.values()), ", ".join(sorted(srcs))
 
 
 def _cgroup_quota_cpus():

@@ -66,7 +66,10 @@ def pmc(dirs, out):
 def main():
     src, out = sys.argv[1], sys.argv[2]
     ks = kernel_stats(os.path.join(src, "ktrace"), out + "_ktrace_stats.csv")
-    passes = [p for p in sorted(glob.glob(os.path.join(src, "*"))) if os.path.isdir(p) and not p.endswith("ktrace")]
+    if os.path.isdir(os.path.join(src, "ktrace_all")):  # every sub-line of the bench, beside the headline alone
+        kernel_stats(os.path.join(src, "ktrace_all"), out + "_ktrace_stats_all.csv")
+    passes = [p for p in sorted(glob.glob(os.path.join(src, "*")))
+              if os.path.isdir(p) and not os.path.basename(p).startswith("ktrace")]
     pm = pmc(passes, out + "_pmc.csv") if passes else []
     for r in ks[:3]:
         print(r[0].split("(")[0], r[1], f"avg {r[3]:.1f} us")
