@@ -573,7 +573,7 @@ def main():
     impl_fpmul = head.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING
     roof = roofline(impl_fpmul, agg_ms, "the GT submission: k_agg_prologue, k_verify_sig beside the GT fold "
                     "(k_gt_plan, k_gt_chunks, k_gt_combine), k_gt_compare",
-                    r"k_agg_prologue|k_gt_(plan|chunks|combine|compare)|k_verify_sig",
+                    r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare)|k_verify_sig<4, true>",
                     f"implemented work: {head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 "
                     f"product each) + {n} x {FPMUL_PER_SIG_PAIRING} Fp-mul (one pairing + final exponentiation "
                     f"per check), x {MADS_PER_FPMUL} u32 mads")
@@ -587,11 +587,11 @@ def main():
                          f"(G2 addition) + {FPMUL_PER_CHECK} (two-pairing check), x {MADS_PER_FPMUL} u32 mads; mean "
                          f"{head.signers.mean():.1f} set bits",
                  "note": "work the GT path does not run is credited here; not a fraction of any peak"}
-    roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph_seq["verify"], "k_verify_sig", r"k_verify_sig",
+    roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph_seq["verify"], "k_verify_sig", r"k_verify_sig<4, false>",
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
                            "+ final exponentiation, oracle op count); kernel alone (fold not beside it)")
     roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph_seq["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
-                         r"k_gt_(plan|chunks|combine)",
+                         r"k_gt_(plan<16>|chunks|combine)",
                          f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each); "
                          "kernels alone (not beside the pairing kernel)")
     roof["kernels_alone_ms"] = {"fold": round(ph_seq["fold"], 4), "k_verify": round(ph_seq["verify"], 4),
@@ -664,7 +664,7 @@ def main():
             "kernels_ms": {k: round(v, 4) for k, v in fph.items() if v is not None},
             "roofline": roofline(full.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING, fph["submit"],
                                  "the GT submission (as the headline)",
-                                 r"k_agg_prologue|k_gt_(plan|chunks|combine|compare)|k_verify_sig",
+                                 r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare)|k_verify_sig<4, true>",
                                  f"implemented work: {full.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul + "
                                  f"{n} x {FPMUL_PER_SIG_PAIRING} Fp-mul, x {MADS_PER_FPMUL} u32 mads")}
         del full
