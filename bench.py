@@ -675,11 +675,6 @@ def main():
             # a verifier serving a continuous stream: batches in flight on several
             # HIP streams, one engine context (own workspaces) per stream
             engs = [eng] + [Engine(device=local_dev, flavor="go") for _ in range(args.pipeline - 1)]
-            # with several batches in flight, each batch's fold runs before its
-            # pairing kernel: the other batch's kernels fill the gaps
-            # (profiles/r03h_pipeline_ab.json: 4.36 vs 4.23 M/s for two batches)
-            for e in engs:
-                e.set_fold_overlap(False)
             for e in engs[1:]:
                 assert e.set_message(LIB_MESSAGE) == 0
                 assert not e.registry_load(head.reg).any()
@@ -698,7 +693,6 @@ def main():
                                   "unit": "verifications/s", "batches_in_flight": len(engs), "batch": n,
                                   "ms_per_step": round(pdt / args.steps * 1e3, 4),
                                   "note": "headline batch on each of the streams; throughput with batches overlapped"}
-            eng.set_fold_overlap(True)
             for e in engs[1:]:
                 e.close()
 

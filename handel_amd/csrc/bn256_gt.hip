@@ -23,7 +23,8 @@
 // Team layouts: k_gt_keys / k_verify_sig use the pairing team region of
 // k_verify (bn256_pairing.h); the fold kernels use the compact FOLD region of
 // the generator (slots F, A, B, registers ZERO and ONE, pre-pass scratch:
-// kFoldTeamElems elements), so several fold waves share a SIMD.
+// kFoldTeamElems elements: 9.6 KB per 4-team workgroup), so several fold
+// waves share a SIMD, also beside k_verify_sig's waves.
 #include <hip/hip_runtime.h>
 
 #include "bn256_agg.h"
@@ -647,11 +648,18 @@ HG_DEV bool t12_equal(const Team& T, int a, int b) {
 // FE(Miller(G2Base at -sig)) == Y_r  <=>  e(H, agg) * e(-sig, G2Base) == 1
 // kStore: write FE(Miller(G2Base at -sig)) to fe[r] instead (the fold runs
 // beside this kernel on a second stream; k_gt_compare finishes the check)
+// The team region ends after the last element the sig-only Miller loop and
+// the final exponentiation touch (kSigTeamElems, from the generator: slots F..L
+// and the FE pre-pass scratch, no pk-side G2 registers): 28.5 KB of LDS per
+// 4-team wave instead of k_verify's 33.9 KB, so four fold workgroups (9.6 KB
+// each) fit on a CU beside its four pairing waves.
+static constexpr int kSigTeamWords = kSigTeamElems * 10;
+static_assert(kSigTeamWords % 2 == 0 && kSigTeamWords <= kTeamWords, "sig team region");
 template <int TEAMS, bool kStore>
 __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y,
                                                    Gt* fe, int32_t* codes) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
-  Team T = make_team(lds, kTeamWords);
+  __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kSigTeamWords];
+  Team T = make_team(lds, kSigTeamWords);
   uint32_t* F = team_regs(T);
   const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
   const bool valid = idx < n;

@@ -1185,7 +1185,35 @@ def check_instances(X, seed=3):
                 assert mem[fb + r] == v, f"instance {name} reg {r}"
 
 
+# the programs k_verify_sig runs (bn256_gt.hip: the sig-only Miller loop and
+# the final exponentiation); its team region ends after the last element they
+# (and the hand-written helpers: registers up to FC) touch
+SIG_PROGRAMS = ("SDBL", "LFEV", "FEVAL", "LINE_FIX", "MUL12", "CYC_SQR_X")
+
+
+def touched(bx):
+    """Largest team element index a bound round reads or writes."""
+    m = 0
+    for L in bx.lanes:
+        idx = [L["dst"], L.get("dst2", NONE)] + [d for d, _ in L["pre"]]
+        idx += [s_ for _, t in L["pre"] for s_, _ in t]
+        for pk, lk in (("prod", "lin"), ("prod2", "lin2")):
+            idx += [u for u, v in L.get(pk, [])] + [v for u, v in L.get(pk, [])] + [s_ for s_, _ in L.get(lk, [])]
+        m = max([m] + [v for v in idx if v != NONE])
+    return m
+
+
 def emit_x(X, path):
+    sig_end = F_BASE + REG["FC.y"] + 1  # team_miller_sig's registers: ZERO .. FC
+    fold_end = FOLD_F_BASE + 2           # ZERO, ONE
+    for name, binding in INSTANCES:
+        ctx = X_PROGRAMS[name]
+        for xr in X[name]:
+            t = touched(bind(xr, binding, ctx)) + 1
+            if name in SIG_PROGRAMS and ctx in ("FE", "ML"):
+                sig_end = max(sig_end, t)
+            if ctx == "FOLD":
+                fold_end = max(fold_end, t)
     lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
              "// Two-phase team programs executed by bn256_xprog.h (encoding: see there),",
              "// one table per call-site instance (absolute team element indices).",
@@ -1194,7 +1222,8 @@ def emit_x(X, path):
              "enum XProg { " + ", ".join(f"XP_{n}" for n in X_PROGRAMS) + " };",
              f"static constexpr int kXFetchWords = {X_FETCH_WORDS};",
              f"static constexpr int kFoldRegBase = {FOLD_F_BASE};  // FOLD team region: ZERO, ONE here",
-             f"static constexpr int kFoldTeamElems = {REGION_END['FOLD']};",
+             f"static constexpr int kFoldTeamElems = {fold_end + fold_end % 2};  // elements the fold programs touch",
+             f"static constexpr int kSigTeamElems = {sig_end + sig_end % 2};  // k_verify_sig's team region",
              "template <int PROG, int D = -1, int A = -1, int B = -1> struct XInst;"]
     words = []
     for name, binding in INSTANCES:
