@@ -64,8 +64,9 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
 // FE(Miller(G2Base at -sig_r)) == y[r] for every request still HG_OK
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s);
 // the same check in two launches, so the fold can run beside the pairing:
-// fe[r] = FE(Miller(G2Base at -sig_r)), then fe[r] == y[r] where still HG_OK
-void launch_sig_pairing(const PointG1* sigs, int n, const LineCoef* tab, Gt* fe, hipStream_t s);
+// fe[r] = FE(Miller(G2Base at -sig_r)) from the 64-byte marshals (decoded in
+// the kernel), then fe[r] == y[r] where still HG_OK
+void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s);
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s);
 
 }  // namespace hg

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bn256_agg.h"
+#include "bn256_decode.h"
 #include "bn256_gt.h"
 #include "bn256_pairing.h"
 
@@ -655,16 +656,23 @@ HG_DEV bool t12_equal(const Team& T, int a, int b) {
 // each) fit on a CU beside its four pairing waves.
 static constexpr int kSigTeamWords = kSigTeamElems * 10;
 static_assert(kSigTeamWords % 2 == 0 && kSigTeamWords <= kTeamWords, "sig team region");
+// kStore: the signature is decoded here from its marshal (sig_bytes, the
+// flavor's rules): the prologue that decodes it for the verdict codes runs on
+// the side stream, off this kernel's critical path. A signature that fails to
+// decode gives a meaningless FE value, which k_gt_compare never reads (its code
+// is the decode error already).
 template <int TEAMS, bool kStore>
-__global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y,
-                                                   Gt* fe, int32_t* codes) {
+__global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const uint8_t* sig_bytes, int flavor, int n,
+                                                   const LineCoef* tab, const Gt* y, Gt* fe, int32_t* codes) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kSigTeamWords];
   Team T = make_team(lds, kSigTeamWords);
   uint32_t* F = team_regs(T);
   const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
   const bool valid = idx < n;
   const int ci = valid ? idx : n - 1;
-  const PointG1 sg = sigs[ci];
+  PointG1 sg;
+  if (kStore) (void)decode_g1_one(sig_bytes + (size_t)ci * 64, flavor, sg);
+  else sg = sigs[ci];
   XStream S = x_stream();
   team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, final_exp_hint());
   team_final_exp(T, F, S);
@@ -724,10 +732,10 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
   k_gt_combine<<<n, 64, 0, s>>>(n, w.hdr, w.multi, w.plan, w.partial, y);
 }
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
-  if (n > 0) k_verify_sig<4, false><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, y, nullptr, codes);
+  if (n > 0) k_verify_sig<4, false><<<nblk(n, 4), 64, 0, s>>>(sigs, nullptr, 0, n, tab, y, nullptr, codes);
 }
-void launch_sig_pairing(const PointG1* sigs, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
-  if (n > 0) k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(sigs, n, tab, nullptr, fe, nullptr);
+void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
+  if (n > 0) k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
 }
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s) {
   if (n > 0) k_gt_compare<<<n, 64, 0, s>>>(fe, y, n, codes);

@@ -744,16 +744,16 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
       HG_CHECK(c, ensure_side(c));
       HG_CHECK(c, c->gt_fe.ensure(n));
     }
-    launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, c->pts1.p, d_codes, (int*)gw.hdr,
-                        (int)(sizeof(GtHdr) / sizeof(int)), s);
     if (overlap) {
-      // s: prologue -> pairing ............ -> wait -> compare
-      // side:          wait -> plan, chunks, combine -> join
+      // s:    pairing (decodes its signatures) ............ -> wait -> compare
+      // side: wait -> prologue (codes, counters), plan, chunks, combine -> join
       HG_CHECK(c, hipEventRecord(c->ev_fork, s));
       PhaseTimer t(c, HG_PHASE_VERIFY, s);
-      launch_sig_pairing(c->pts1.p, (int)n, c->d_lines, c->gt_fe.p, s);
+      launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, c->gt_fe.p, s);
       t.stop();
       HG_CHECK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, c->pts1.p, d_codes, (int*)gw.hdr,
+                          (int)(sizeof(GtHdr) / sizeof(int)), c->side);
       PhaseTimer fold(c, HG_PHASE_AGGREGATE, c->side);
       launch_gt_fold(d_reqs, (int)n, d_words, d_codes, (int)c->nreg, c->block_levels,
                      level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, false, c->side);
@@ -767,6 +767,8 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
       HG_CHECK(c, sub.finish());
       return HG_OK;
     }
+    launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, c->pts1.p, d_codes, (int*)gw.hdr,
+                        (int)(sizeof(GtHdr) / sizeof(int)), s);
     PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
     launch_gt_fold(d_reqs, (int)n, d_words, d_codes, (int)c->nreg, c->block_levels,
                    level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, false, s);
