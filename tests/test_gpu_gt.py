@@ -368,3 +368,32 @@ def test_random_batches_match_oracle(engine, seed, n_reg, m):
     want = _oracle(msg, reg, reqs, words, sigs)
     assert list(got) == list(want)
     assert (got == 0).any() or m < 8
+
+
+def test_policy_switches_on_the_crossing_batch():
+    """Device-stream order of the volume policy: the batch that takes a
+    message past 16384 requests builds the 8-key tables inside its own
+    submission and already runs on them; every batch's verdicts are the
+    expected ones, before and after."""
+    code = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, %r)
+import bench
+from handel_amd.engine import Engine
+e = Engine(device=0, flavor="go")
+assert e.set_message(bench.LIB_MESSAGE) == 0
+reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(e, 1000, 4096, seed=13)
+levels, ok = [], []
+for i in range(6):   # 24576 requests: the threshold is crossed on the 4th batch
+    c = e.verify_aggregate(reqs, words, sigs)
+    ok.append(bool(np.array_equal(c, expect)))
+    levels.append(e.aggregate_tables())
+print(json.dumps({"ok": ok, "levels": levels}))
+""" % ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("HG_GT_LEVEL", "HG_AGG_PATH")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"] == [True] * 6
+    assert out["levels"] == [0, 0, 0, 1, 1, 1]
