@@ -71,6 +71,8 @@ MADS_PER_FPMUL = 136
 # waves per SIMD (profiles/r01_intrate.jsonl: 34.95 T/s; half the VALU rate:
 # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 2 = 39.3 T/s spec-derived).
 P_MAD_TOPS = 34.95
+# HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured)
+P_HBM_GBS = 8000.0
 
 
 def seeded_scalars(n: int, seed: int) -> bytes:
@@ -141,6 +143,35 @@ def make_aggregate_batch(eng: Engine, n_reg: int, n: int, seed: int, full: bool 
     expect = _tamper(eng, sigs, n)
     return (np.array(reqs, dtype=REQ_DTYPE), np.array(words, dtype=np.uint64), bytes(sigs), expect,
             np.array(signers), reg)
+
+
+def requests_as_packets(reqs, words, sigs: bytes, n_reg: int, seed: int):
+    """The wire packets (net.go:34-44) that carry these aggregate requests to
+    a receiving instance: for request i, a receiver whose level range is the
+    request's (the sibling block of the range), that level, a sender inside
+    the range, and the MultiSignature marshal of its bitset and signature
+    (crypto.go:65-82). Returns (pool, hg_packet records)."""
+    from handel_amd import partitioner as HP
+    from handel_amd.packets import Packet, pack_packets
+
+    rng = np.random.default_rng(seed)
+    pkts, recv = [], []
+    for i, (off, bitlen, size, woff) in enumerate(reqs.tolist()):
+        bits = HP.words_to_bits(words[woff:woff + (bitlen + 63) // 64], bitlen)
+        for k in range(HP.log2_ceil(n_reg)):
+            node = off ^ (1 << k)
+            if node < n_reg:
+                try:
+                    if HP.range_level(node, n_reg, k + 1) == (off, off + size):
+                        break
+                except HP.PartitionerError:
+                    pass
+        else:
+            raise ValueError(f"request {i} is not a Handel level range")
+        pkts.append(Packet(int(rng.integers(off, off + size)), k + 1,
+                           HP.multisig_marshal(bits, sigs[64 * i:64 * i + 64])))
+        recv.append(node)
+    return pack_packets(pkts, recv)
 
 
 def gt_fold_terms(reqs, words, n_reg: int) -> int:
@@ -472,6 +503,61 @@ def handel_run_volume(dev, stream, device: int, n_reg: int = 2000, requests: int
     return out
 
 
+def packet_intake(eng: Engine, head, n_reg: int, dev, stream, timer, args, world: int):
+    """Handel.NewPacket's parse step on the device (hg_parse_packets_device):
+    the headline's 4096 requests as the wire packets that carry them, in HBM;
+    'parse' = packets -> verification requests, 'parse_verify' = packets ->
+    verdicts (parse, then the headline's GT submission on the parsed slots)."""
+    n = len(head.reqs)
+    pool, recs = requests_as_packets(head.reqs, head.words, head.sigs, n_reg, seed=99)
+    stride = eng.packet_stride_words()
+    d_pool = _dev_bytes(pool, dev)
+    d_pkts = _dev_bytes(recs.tobytes(), dev)
+    d_reqs = torch.zeros(2 * n * REQ_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_words = torch.zeros(2 * n * stride, dtype=torch.int64, device=dev)
+    d_sigs = torch.zeros(2 * n * 64, dtype=torch.uint8, device=dev)
+    d_pcodes = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    codes = torch.zeros(n, dtype=torch.int32, device=dev)
+    s = stream.cuda_stream
+
+    def parse():
+        eng.parse_packets_device(d_pool.data_ptr(), len(pool), d_pkts.data_ptr(), n, stride, d_reqs.data_ptr(),
+                                 d_words.data_ptr(), d_sigs.data_ptr(), d_pcodes.data_ptr(), s)
+
+    def parse_verify():
+        parse()
+        eng.verify_aggregate_device(d_reqs.data_ptr(), n, d_words.data_ptr(), d_sigs.data_ptr(), codes.data_ptr(), 0,
+                                    s)
+
+    pdt = timer.run(parse, args.steps, args.warmup)
+    assert (d_pcodes[:n] == 0).all().item(), "every headline packet parses"
+    vdt = timer.run(parse_verify, args.steps, args.warmup)
+    assert np.array_equal(codes.cpu().numpy(), head.expect), "verdicts from parsed packets"
+    # the parse kernel alone, HIP events on its stream
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 20
+    ev[0].record(stream)
+    for _ in range(reps):
+        parse()
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    k_ms = ev[0].elapsed_time(ev[1]) / reps
+    moved = len(pool) + recs.nbytes + 2 * n * (REQ_DTYPE.itemsize + 8 * stride + 64 + 4)
+    achieved = moved / (k_ms * 1e-3) / 1e9
+    return {"metric": "Handel packets parsed/sec (batch 4096)", "value": round(n * args.steps * world / pdt, 1),
+            "unit": "packets/s", "ms_per_step": round(pdt / args.steps * 1e3, 4),
+            "parse_verify": {"value": round(n * args.steps * world / vdt, 1), "unit": "verifications/s",
+                             "ms_per_step": round(vdt / args.steps * 1e3, 4),
+                             "what": "wire packets in HBM -> parse -> GT submission -> verdicts"},
+            "workload": f"the headline's {n} requests as wire packets ({len(pool)} B), receiver and level per packet",
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": P_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved / P_HBM_GBS, 4), "traffic": None, "kernel": "k_parse_packets",
+                         "kernel_ms": round(k_ms, 4),
+                         "work": f"bytes per launch: pool {len(pool)} + records {recs.nbytes} + 2 slots x "
+                                 f"(request 16 + {stride} words x 8 + signature 64 + code 4) per packet",
+                         "note": "a 4096-packet launch is launch/latency bound; the fraction says so"}}
+
+
 def timed_phases(eng: Engine, run):
     """Runs run() with the engine's HIP-event timing on; returns per-phase
     (mean ms per interval) for verify / aggregate fold / whole submission."""
@@ -696,6 +782,7 @@ def main():
             for e in engs[1:]:
                 e.close()
 
+        extra["packet_intake"] = packet_intake(eng, head, n_reg, dev, stream, timer, args, world)
         extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)
 
     cpu = None

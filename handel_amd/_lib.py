@@ -30,6 +30,17 @@ HG_ERR_SIG_CF_EXCEEDS = 10
 HG_ERR_SIG_CF_MALFORMED = 11
 HG_ERR_SIG_CF_SHORT = 12
 HG_ERR_MULTI_SIZES = 13
+HG_ERR_PKT_ORIGIN = 20
+HG_ERR_PKT_LEVEL = 21
+HG_ERR_PKT_EOF = 22
+HG_ERR_PKT_UNEXPECTED_EOF = 23
+HG_ERR_PKT_BITSET_SHORT = 24
+HG_ERR_PKT_TYPE_MISMATCH = 25
+HG_ERR_PKT_BITSET_SIZE = 26
+HG_ERR_PKT_NO_SIG = 27
+HG_ERR_PKT_ID_RANGE = 28
+HG_PKT_NO_IND = 29
+HG_PKT_HAS_IND = 1
 HG_ERR_ARG = 100
 HG_ERR_DEVICE = 101
 
@@ -84,6 +95,10 @@ SIGNATURES = {
     "hg_timing_read_phase": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
     "hg_sync": (_I, [_P]),
     "hg_context_bytes": (_SZ, [_P]),
+    "hg_packet_stride_words": (_SZ, [_P]),
+    "hg_parse_packets": (_I, [_P, _P, _SZ, _P, _SZ, _SZ, _P, _P, _P, _P]),
+    "hg_parse_packets_device": (_I, [_P, _P, _SZ, _P, _SZ, _SZ, _P, _P, _P, _P, _P]),
+    "hg_packet_error": (_I, [_P, _I, _P, ctypes.c_char_p, _SZ]),
     "hg_batcher_create": (_I, [_P, _SZ, ctypes.c_uint, ctypes.POINTER(_P)]),
     "hg_batcher_destroy": (None, [_P]),
     "hg_batcher_submit": (_I, [_P, _P, _SZ, _P, _P, _P, ctypes.POINTER(_P)]),

@@ -21,6 +21,7 @@
 
 #include "bn256_gt.h"
 #include "bn256_kernels.h"
+#include "hg_packets.h"
 
 using namespace hg;
 
@@ -172,6 +173,7 @@ struct hg_ctx {
   DevBuf<CheckIn> checks;
   DevBuf<int32_t> codes_a, codes_b, codes_c;
   DevBuf<hg_request> reqs;
+  DevBuf<hg_packet> pkts;  // hg_parse_packets staging
   DevBuf<int> order;       // aggregation schedule (k_agg_order)
   DevBuf<uint8_t> agg_ws;  // per-request fold results (k_aggregate -> k_agg_finish)
   DevBuf<uint64_t> words;
@@ -907,6 +909,16 @@ const char* hg_code_string(int code, int flavor) {
     case HG_ERR_SIG_CF_MALFORMED: return "bn256: multisig can't unmarshal: bn256: malformed point";
     case HG_ERR_SIG_CF_SHORT: return "bn256: multisig can't unmarshal: bn256: not enough data";
     case HG_ERR_MULTI_SIZES: return "verify multisignature: inconsistent sizes";
+    case HG_ERR_PKT_ORIGIN: return "packet's origin out of range";
+    case HG_ERR_PKT_LEVEL: return "invalid packet's level";
+    case HG_ERR_PKT_EOF: return "EOF";
+    case HG_ERR_PKT_UNEXPECTED_EOF: return "unexpected EOF";
+    case HG_ERR_PKT_BITSET_SHORT: return "bitset received smaller than expected";
+    case HG_ERR_PKT_TYPE_MISMATCH: return "unmarshalling error: type mismatch";
+    case HG_ERR_PKT_BITSET_SIZE: return "invalid bitset's size for given level";
+    case HG_ERR_PKT_NO_SIG: return "no signature in the bitset";
+    case HG_ERR_PKT_ID_RANGE: return "globalID outside level's range";
+    case HG_PKT_NO_IND: return "";
     case HG_ERR_ARG: return "invalid argument";
     default: return "device error";
   }
@@ -1398,6 +1410,95 @@ int hg_diag_read(hg_ctx* c, uint64_t* out, size_t n) {
   return diag_read(out, n) == 0 ? HG_OK : HG_ERR_ARG;
 }
 
+// ---------------------------------------------------------------- packet intake
+static bool packet_args_ok(const hg_ctx* c, size_t n, size_t stride) {
+  // slot word offsets (2n slots of `stride` words) are 32-bit
+  return n <= (size_t)INT32_MAX / 2 && stride >= pkt_stride_words(c->nreg) && stride <= (size_t)INT32_MAX &&
+         (n == 0 || 2 * n <= (size_t)UINT32_MAX / stride);
+}
+
+size_t hg_packet_stride_words(hg_ctx* c) {
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  return pkt_stride_words(c->nreg);
+}
+
+int hg_parse_packets_device(hg_ctx* c, const uint8_t* d_pool, size_t pool_len, const hg_packet* d_pkts, size_t n,
+                            size_t stride_words, hg_request* d_reqs, uint64_t* d_words, uint8_t* d_sigs,
+                            int32_t* d_codes, void* stream) {
+  if (!c || (n && (!d_pkts || !d_reqs || !d_words || !d_sigs || !d_codes)) || (pool_len && !d_pool)) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!packet_args_ok(c, n, stride_words)) return HG_ERR_ARG;
+  HG_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  Submission sub(c, s);
+  HG_CHECK(c, sub.start());
+  launch_parse_packets(d_pool, pool_len, d_pkts, (int)n, (uint32_t)c->nreg, c->flavor, (int)stride_words, d_reqs,
+                       d_words, d_sigs, d_codes, s);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, sub.finish());
+  return HG_OK;
+}
+
+int hg_parse_packets(hg_ctx* c, const uint8_t* pool, size_t pool_len, const hg_packet* pkts, size_t n,
+                     size_t stride_words, hg_request* reqs, uint64_t* words, uint8_t* sigs, int32_t* codes) {
+  if (!c || (n && (!pkts || !reqs || !words || !sigs || !codes)) || (pool_len && !pool)) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  for (size_t i = 0; i < n; i++) {
+    const hg_packet& p = pkts[i];
+    if ((uint64_t)p.ms_off + p.ms_len > pool_len ||
+        ((p.flags & HG_PKT_HAS_IND) && (uint64_t)p.ind_off + p.ind_len > pool_len))
+      return HG_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!packet_args_ok(c, n, stride_words)) return HG_ERR_ARG;
+  HG_CHECK(c, hipSetDevice(c->device));
+  const size_t nw = 2 * n * stride_words;
+  HG_CHECK(c, c->bytes_a.ensure(pool_len ? pool_len : 1));
+  HG_CHECK(c, c->bytes_b.ensure(2 * n * 64));
+  HG_CHECK(c, c->pkts.ensure(n));
+  HG_CHECK(c, c->reqs.ensure(2 * n));
+  HG_CHECK(c, c->words.ensure(nw));
+  HG_CHECK(c, c->codes_a.ensure(2 * n));
+  Submission sub(c, c->stream);
+  HG_CHECK(c, sub.start());
+  if (pool_len) HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, pool, pool_len, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->pkts.p, pkts, n * sizeof(hg_packet), hipMemcpyHostToDevice, c->stream));
+  launch_parse_packets(c->bytes_a.p, pool_len, c->pkts.p, (int)n, (uint32_t)c->nreg, c->flavor, (int)stride_words,
+                       c->reqs.p, c->words.p, c->bytes_b.p, c->codes_a.p, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(reqs, c->reqs.p, 2 * n * sizeof(hg_request), hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(words, c->words.p, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(sigs, c->bytes_b.p, 2 * n * 64, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_a.p, 2 * n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, sub.finish());
+  HG_CHECK(c, hipStreamSynchronize(c->stream));
+  return HG_OK;
+}
+
+int hg_packet_error(hg_ctx* c, int code, const hg_packet* p, char* buf, size_t cap) {
+  if (!c || !p || (cap && !buf)) return -1;
+  size_t nreg;
+  int flavor;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    nreg = c->nreg;
+    flavor = c->flavor;
+  }
+  if (code == HG_ERR_PKT_LEVEL) return snprintf(buf, cap, "invalid packet's level %d", (int)p->level);
+  if (code == HG_ERR_PKT_ID_RANGE) {
+    // partitioner.go:113-115 (the receiver's range at the packet's level)
+    uint32_t lo = 0, hi = 0;
+    (void)pkt_range_level(p->receiver, (uint32_t)nreg, (int)p->level, lo, hi);
+    return snprintf(buf, cap, "globalID outside level's range. id=%d, min=%u, max=%u, level=%d", (int)p->origin, lo,
+                    hi, (int)p->level);
+  }
+  return snprintf(buf, cap, "%s", hg_code_string(code, flavor));
+}
+
 size_t hg_context_bytes(hg_ctx* c) {
   if (!c) return 0;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1410,7 +1511,7 @@ size_t hg_context_bytes(hg_ctx* c) {
   b += (c->gt_key.cap + c->gt_w8.cap + c->gt_win.cap + c->gt_blk.cap + c->gt_partial.cap + c->gt_y.cap) * sizeof(Gt);
   b += c->gt_plan.cap * sizeof(GtReq) + c->gt_hdr.cap * sizeof(GtHdr) + c->gt_terms.cap * sizeof(uint32_t);
   b += c->gt_ord.cap * sizeof(int2) + c->gt_multi.cap * sizeof(int) + c->gt_fe.cap * sizeof(Gt);
-  b += c->sub_count.cap * sizeof(int);
+  b += c->sub_count.cap * sizeof(int) + c->pkts.cap * sizeof(hg_packet);
   return b;
 }
 

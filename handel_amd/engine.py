@@ -21,6 +21,9 @@ FLAVORS = {"go": _lib.HG_FLAVOR_GO, "bn256/go": _lib.HG_FLAVOR_GO,
            "cf": _lib.HG_FLAVOR_CF, "bn256/cf": _lib.HG_FLAVOR_CF, "bn256": _lib.HG_FLAVOR_CF}
 
 REQ_DTYPE = np.dtype([("offset", "<u4"), ("bitlen", "<u4"), ("level_size", "<u4"), ("word_offset", "<u4")])
+# hg_packet (include/handel_gpu.h): one received Handel packet, marshals as pool ranges
+PACKET_DTYPE = np.dtype([("origin", "<i4"), ("receiver", "<u4"), ("level", "<u4"), ("flags", "<u4"),
+                         ("ms_off", "<u4"), ("ms_len", "<u4"), ("ind_off", "<u4"), ("ind_len", "<u4")])
 
 
 def _ptr(a) -> Optional[int]:
@@ -172,6 +175,39 @@ class Engine:
                     "hg_verify_aggregate")
         return (codes, agg.tobytes()) if want_agg else codes
 
+    # ------------------------------------------------------------ packet intake
+    def packet_stride_words(self) -> int:
+        """Bitset words per request slot of hg_parse_packets (largest level / 64)."""
+        return int(self.L.hg_packet_stride_words(self.ctx))
+
+    def parse_packets(self, pool, pkts: np.ndarray, stride: Optional[int] = None):
+        """Handel.NewPacket's parse step for n packets (hg_parse_packets):
+        returns (reqs[2n], words, sigs[2n*64], codes[2n]); slot i is packet i's
+        multisignature, slot n + i its individual signature."""
+        pkts = np.ascontiguousarray(pkts, dtype=PACKET_DTYPE)
+        pool = _u8(pool)
+        n = len(pkts)
+        stride = self.packet_stride_words() if stride is None else int(stride)
+        reqs, words, sigs, codes = _parse_outputs(n, stride)
+        self._check(self.L.hg_parse_packets(self.ctx, _ptr(pool) if len(pool) else None, len(pool), _ptr(pkts), n,
+                                            stride, _ptr(reqs), _ptr(words), _ptr(sigs), _ptr(codes)),
+                    "hg_parse_packets")
+        return reqs, words, sigs.tobytes(), codes
+
+    def parse_packets_device(self, d_pool: int, pool_len: int, d_pkts: int, n: int, stride: int, d_reqs: int,
+                             d_words: int, d_sigs: int, d_codes: int, stream: int = 0) -> None:
+        """hg_parse_packets_device on raw device pointers (asynchronous)."""
+        self._check(self.L.hg_parse_packets_device(self.ctx, d_pool or None, pool_len, d_pkts, n, stride, d_reqs,
+                                                   d_words, d_sigs, d_codes, stream or None),
+                    "hg_parse_packets_device")
+
+    def packet_error(self, code: int, pkt) -> str:
+        """The reference's text for a packet code (hg_packet_error)."""
+        p = np.ascontiguousarray(np.asarray(pkt, dtype=PACKET_DTYPE).reshape(1))
+        buf = ctypes.create_string_buffer(256)
+        self.L.hg_packet_error(self.ctx, int(code), _ptr(p), buf, 256)
+        return buf.value.decode()
+
     def verify_aggregate_msg(self, msg: bytes, reqs: np.ndarray, words: np.ndarray, sigs: bytes):
         """verify_aggregate with the message given per call: hashing and the
         batch under one lock hold of the context (hg_verify_aggregate_msg)."""
@@ -299,6 +335,71 @@ class Engine:
 
     def sync(self):
         self._check(self.L.hg_sync(self.ctx), "hg_sync")
+
+
+def _parse_outputs(n: int, stride: int):
+    return (np.zeros(2 * n, dtype=REQ_DTYPE), np.zeros(2 * n * stride, dtype=np.uint64),
+            np.zeros(2 * n * 64, dtype=np.uint8), np.zeros(2 * n, dtype=np.int32))
+
+
+class Batcher:
+    """The native launch-merging queue on one engine (hg_batcher_*): callers
+    (one thread per Handel instance) submit single aggregate requests; a
+    dispatcher thread merges what is queued into one launch per message.
+    The engine must outlive the batcher."""
+
+    def __init__(self, engine: Engine, max_batch: int = 4096, max_wait_us: int = 200):
+        self.engine = engine
+        self.L = engine.L
+        h = ctypes.c_void_p()
+        rc = self.L.hg_batcher_create(engine.ctx, max_batch, max_wait_us, ctypes.byref(h))
+        if rc != 0:
+            raise HandelGPUError(f"hg_batcher_create: code {rc}")
+        self.b = h
+
+    def close(self):
+        if getattr(self, "b", None):
+            self.L.hg_batcher_destroy(self.b)
+            self.b = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit(self, msg: bytes, offset: int, bitlen: int, level_size: int, words, sig: bytes) -> int:
+        """Queues one request (hg_batcher_submit); returns the ticket handle."""
+        m = _u8(msg)
+        req = np.array([(offset, bitlen, level_size, 0)], dtype=REQ_DTYPE)
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        sg = _u8(sig)
+        if len(sg) != 64:
+            raise ValueError("signature must be 64 bytes")
+        t = ctypes.c_void_p()
+        rc = self.L.hg_batcher_submit(self.b, _ptr(m) if len(m) else None, len(m), _ptr(req),
+                                      _ptr(w) if len(w) else None, _ptr(sg), ctypes.byref(t))
+        if rc != 0:
+            raise HandelGPUError(f"hg_batcher_submit: code {rc}")
+        return t.value
+
+    def wait(self, ticket: int) -> int:
+        """The request's hg_code (hg_batcher_wait); releases the ticket."""
+        code = ctypes.c_int32(-1)
+        rc = self.L.hg_batcher_wait(self.b, ctypes.c_void_p(ticket), ctypes.byref(code))
+        if rc != 0:
+            raise HandelGPUError(f"hg_batcher_wait: code {rc}")
+        return int(code.value)
+
+    def verify(self, msg: bytes, offset: int, bitlen: int, level_size: int, words, sig: bytes) -> int:
+        """One processing.go verifySignature through the queue (blocking)."""
+        return self.wait(self.submit(msg, offset, bitlen, level_size, words, sig))
+
+    def stats(self) -> Tuple[int, int]:
+        """(batches launched, requests verified) so far."""
+        b, r = ctypes.c_uint64(), ctypes.c_uint64()
+        self.L.hg_batcher_stats(self.b, ctypes.byref(b), ctypes.byref(r))
+        return b.value, r.value
 
 
 def requests_array(items: Sequence[Tuple[int, int, int, int]]) -> np.ndarray:

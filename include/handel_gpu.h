@@ -46,6 +46,20 @@ enum hg_code {
   HG_ERR_SIG_CF_MALFORMED = 11, /* "bn256: multisig can't unmarshal: bn256: malformed point" */
   HG_ERR_SIG_CF_SHORT = 12,     /* "bn256: multisig can't unmarshal: bn256: not enough data" */
   HG_ERR_MULTI_SIZES = 13,  /* "verify multisignature: inconsistent sizes"  crypto.go:122-124 */
+  /* Handel packet intake (hg_parse_packets): handel.go:371-436 validatePacket /
+   * parseSignatures, crypto.go:86-110 MultiSignature.Unmarshal, bitset.go:166-177
+   * WilffBitSet.UnmarshalBinary over willf/bitset v1.1.10 ReadFrom */
+  HG_ERR_PKT_ORIGIN = 20,        /* "packet's origin out of range"              handel.go:374-376 */
+  HG_ERR_PKT_LEVEL = 21,         /* "invalid packet's level %d"                 handel.go:378-383 */
+  HG_ERR_PKT_EOF = 22,           /* "EOF" (encoding/binary.Read on no bytes)    crypto.go:89, bitset.go:169 */
+  HG_ERR_PKT_UNEXPECTED_EOF = 23, /* "unexpected EOF" (binary.Read, short read) */
+  HG_ERR_PKT_BITSET_SHORT = 24,  /* "bitset received smaller than expected"     crypto.go:93-96 */
+  HG_ERR_PKT_TYPE_MISMATCH = 25, /* "unmarshalling error: type mismatch"        willf ReadFrom */
+  HG_ERR_PKT_BITSET_SIZE = 26,   /* "invalid bitset's size for given level"     handel.go:398-401 */
+  HG_ERR_PKT_NO_SIG = 27,        /* "no signature in the bitset"                handel.go:402-405 */
+  HG_ERR_PKT_ID_RANGE = 28,      /* "globalID outside level's range. id=%d, min=%d, max=%d, level=%d"
+                                    partitioner.go:107-119 IndexAtLevel, handel.go:421-425 */
+  HG_PKT_NO_IND = 29,            /* not an error: the packet carried no individual signature */
   HG_ERR_ARG = 100,         /* bad argument to this API */
   HG_ERR_DEVICE = 101       /* HIP runtime failure (see hg_last_error) */
 };
@@ -247,6 +261,53 @@ int hg_sync(hg_ctx* ctx);
 /* Device memory held by the context (registry, its sums, GT tables,
  * workspaces), in bytes: the HBM one simul process's verifier costs. */
 size_t hg_context_bytes(hg_ctx* ctx);
+
+/* ---------------------------------------------------------------- packet intake
+ * Handel.NewPacket's parse step for a batch of received packets (handel.go:
+ * 127-152 -> validatePacket :371-385 -> parseSignatures :389-436): the origin
+ * and level checks against the RECEIVING instance's partitioner
+ * (partitioner.go:95-178), MultiSignature.Unmarshal of the wire bytes
+ * (crypto.go:86-110: u16 BE blob length, the WilffBitSet blob = u16 BE bit
+ * length + willf's u64 BE length and u64 BE words, then the signature
+ * marshal), the bit-length and empty-bitset checks, and the optional
+ * individual signature with its IndexAtLevel check. The output is the
+ * verification requests processing.go's verifySignature runs on
+ * (hg_verify_aggregate*), already in HBM for the device variant. */
+typedef struct {
+  int32_t origin;     /* Packet.Origin (net.go:36) */
+  uint32_t receiver;  /* id of the Handel instance that received it (its partitioner) */
+  uint32_t level;     /* Packet.Level (net.go:39; a byte on the wire) */
+  uint32_t flags;     /* HG_PKT_HAS_IND: Packet.IndividualSig is non-nil */
+  uint32_t ms_off, ms_len;   /* Packet.MultiSig = pool[ms_off .. ms_off + ms_len) */
+  uint32_t ind_off, ind_len; /* Packet.IndividualSig = pool[ind_off .. ind_off + ind_len) */
+} hg_packet;
+#define HG_PKT_HAS_IND 1u
+/* Words of bitset per request slot: ceil(largest level size / 64) for the
+ * context's registry (the largest level holds 2^(ceil(log2 N) - 1) ids). */
+size_t hg_packet_stride_words(hg_ctx* ctx);
+/* Parses n packets against the context's registry size and flavor. Outputs
+ * have 2n slots: slot i is packet i's multisignature, slot n + i its
+ * individual signature as a one-bit multisignature of the level (handel.go:
+ * 414-433). reqs[2n] (word_offset = slot * stride_words), words[2n *
+ * stride_words] (bits at or above the bit length cleared), sigs[2n * 64] (the
+ * signature marshal's first 64 bytes), codes[2n]: codes[i] = HG_OK or the
+ * packet's first error in the reference's order; codes[n + i] = codes[i] if
+ * that is an error, else HG_OK or HG_PKT_NO_IND. A packet whose individual
+ * signature fails fails as a whole (parseSignatures returns the error and
+ * NewPacket drops both). stride_words must be >= hg_packet_stride_words;
+ * every pool range must lie inside pool_len (else HG_ERR_ARG). */
+int hg_parse_packets(hg_ctx* ctx, const uint8_t* pool, size_t pool_len, const hg_packet* pkts, size_t n,
+                     size_t stride_words, hg_request* reqs, uint64_t* words, uint8_t* sigs, int32_t* codes);
+/* Device-resident variant (pool, pkts and every output on the device);
+ * asynchronous on `stream`. A packet whose range leaves the pool gets
+ * HG_ERR_ARG in its codes instead of a read outside it. */
+int hg_parse_packets_device(hg_ctx* ctx, const uint8_t* d_pool, size_t pool_len, const hg_packet* d_pkts, size_t n,
+                            size_t stride_words, hg_request* d_reqs, uint64_t* d_words, uint8_t* d_sigs,
+                            int32_t* d_codes, void* stream);
+/* The exact text the reference logs for packet p's code (with the level and
+ * range values of the formatted errors), NUL-terminated into buf; returns the
+ * full length (snprintf convention). */
+int hg_packet_error(hg_ctx* ctx, int code, const hg_packet* p, char* buf, size_t cap);
 
 /* ---------------------------------------------------------------- batcher
  * A launch-merging request queue on one context, for callers that verify one

@@ -924,3 +924,105 @@ def verify_multisignature(registry_pks: Sequence, bits: Sequence[bool], sig, msg
     if status == "nil":
         return ERR_EMPTY_AGGREGATE
     return (verify_signature_fast if fast else verify_signature)(agg, msg, sig)
+
+
+# ---------------------------------------------------------------------------
+# Handel packet intake: Handel.NewPacket's parse step (handel.go:127-152)
+# ---------------------------------------------------------------------------
+ERR_PKT_ORIGIN = "packet's origin out of range"                 # handel.go:374-376
+ERR_PKT_LEVEL = "invalid packet's level %d"                     # handel.go:378-383
+ERR_PKT_BITSET_SHORT = "bitset received smaller than expected"  # crypto.go:93-96
+ERR_PKT_TYPE_MISMATCH = "unmarshalling error: type mismatch"    # willf/bitset v1.1.10 ReadFrom
+ERR_PKT_BITSET_SIZE = "invalid bitset's size for given level"   # handel.go:398-401
+ERR_PKT_NO_SIG = "no signature in the bitset"                   # handel.go:402-405
+ERR_PKT_ID_RANGE = "globalID outside level's range. id=%d, min=%d, max=%d, level=%d"  # partitioner.go:113-115
+ERR_READ_EOF = "EOF"
+ERR_READ_UNEXPECTED_EOF = "unexpected EOF"
+
+
+def _short_read(avail: int) -> str:
+    """encoding/binary.Read -> io.ReadFull: EOF when nothing could be read,
+    ErrUnexpectedEOF on a partial read (Go stdlib, restated)."""
+    return ERR_READ_EOF if avail == 0 else ERR_READ_UNEXPECTED_EOF
+
+
+def sig_unmarshal_error(m: bytes, flavor: str) -> Optional[str]:
+    """SigBLS.UnmarshalBinary's error text (bn256/go/bn256.go:182-190,
+    bn256/cf/bn256.go:183-190: cloudflare's G1 error wrapped)."""
+    _, e = g1_unmarshal(m, flavor)
+    if e is None:
+        return None
+    return e if flavor == "go" else "bn256: multisig can't unmarshal: " + e
+
+
+def parse_packet(nreg: int, flavor: str, receiver: int, origin: int, level: int, ms: bytes,
+                 ind: Optional[bytes] = None) -> dict:
+    """The packet checks of Handel.NewPacket at the instance `receiver` of a
+    registry of nreg ids: validatePacket (handel.go:371-385), then
+    parseSignatures (handel.go:389-436) with MultiSignature.Unmarshal
+    (crypto.go:86-110), WilffBitSet.UnmarshalBinary (bitset.go:166-177) and
+    willf/bitset v1.1.10's ReadFrom (upstream, restated: u64 BE length,
+    New(length), binary.Read of wordsNeeded(length) u64 BE words; a make() of
+    more than 2^48 bytes panics inside New, which recovers to an empty set, so
+    ReadFrom reports a length mismatch). ind: Packet.IndividualSig (None = nil).
+
+    Returns {"err": text or None, "range": (lo, hi), "bitlen": w.l, "bits": the
+    set bits below w.l as an int (BitSet.Get), "sig": the signature bytes,
+    "ind_bit": the individual's level index or None}."""
+    out = {"err": None, "range": (0, 0), "bitlen": 0, "bits": 0, "sig": b"", "ind_bit": None}
+
+    def fail(e):
+        out["err"] = e
+        return out
+
+    if origin < 0 or origin >= nreg:
+        return fail(ERR_PKT_ORIGIN)
+    # createLevels: the receiver's Partitioner.Levels() = 1..MaxLevel with a non-empty range
+    rng, e = range_level(receiver, nreg, level) if 1 <= level <= log2_ceil(nreg) else (None, "no level")
+    if e is not None:
+        return fail(ERR_PKT_LEVEL % level)
+    lo, hi = rng
+    out["range"] = (lo, hi)
+    if len(ms) < 2:
+        return fail(_short_read(len(ms)))
+    length = int.from_bytes(ms[0:2], "big")
+    blob = ms[2:2 + length]
+    if len(blob) < length:
+        return fail(ERR_PKT_BITSET_SHORT)
+    if len(blob) < 2:
+        return fail(_short_read(len(blob)))
+    wl = int.from_bytes(blob[0:2], "big")
+    out["bitlen"] = wl
+    rest = blob[2:]
+    if len(rest) < 8:
+        return fail(_short_read(len(rest)))
+    flen = int.from_bytes(rest[0:8], "big")
+    cap = (1 << 64) - 1
+    need = (cap >> 6) if flen > cap - 64 + 1 else (flen + 63) >> 6  # willf wordsNeeded
+    if need * 8 > 1 << 48:
+        return fail(ERR_PKT_TYPE_MISMATCH)
+    avail = len(rest) - 8
+    if need > 0 and avail < 8 * need:
+        return fail(_short_read(avail))
+    fwords = [int.from_bytes(rest[8 + 8 * j:16 + 8 * j], "big") for j in range(need)]
+    sig = ms[2 + length:]
+    e = sig_unmarshal_error(sig, flavor)
+    if e is not None:
+        return fail(e)
+    out["sig"] = sig[:64]
+    if wl != hi - lo:
+        return fail(ERR_PKT_BITSET_SIZE)
+    if all(w == 0 for w in fwords):  # willf None(): whole words
+        return fail(ERR_PKT_NO_SIG)
+    v = 0
+    for j, w in enumerate(fwords):
+        v |= w << (64 * j)
+    out["bits"] = v & ((1 << min(wl, flen)) - 1)  # Get(i): i < w.l and i < willf's length
+    if ind is not None:
+        e = sig_unmarshal_error(ind, flavor)
+        if e is not None:
+            return fail(e)
+        if not lo <= origin < hi:  # IndexAtLevel (partitioner.go:107-119)
+            return fail(ERR_PKT_ID_RANGE % (origin, lo, hi, level))
+        out["ind_bit"] = origin - lo
+    return out

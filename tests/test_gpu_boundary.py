@@ -304,3 +304,48 @@ def test_sharded_verification_two_ranks_one_gpu():
     res = sorted(q.get(timeout=10) for _ in range(world))
     assert [r[1] for r in res] == [True, True]
     assert res[0][2] == res[1][2] == 1000 - 125
+
+
+def test_native_batcher_two_messages_threads(engine):
+    """hg_batcher_*: 16 threads each verify their own requests one at a time
+    (a Handel instance's processLoop) on two interleaved messages; every
+    verdict is the one-batch result of hg_verify_aggregate_msg for its
+    message, and concurrent requests were merged into fewer launches."""
+    import threading
+
+    import bench
+    from handel_amd.engine import Batcher
+
+    n_reg, n = 300, 96
+    msgs = [bench.LIB_MESSAGE, b"Peaches and Cream"]
+    assert engine.set_message(msgs[0]) == 0
+    reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(engine, n_reg, n, seed=31)
+    want = [engine.verify_aggregate_msg(m, reqs, words, sigs) for m in msgs]
+    assert np.array_equal(want[0], expect) and (want[1] != 0).all()
+    b = Batcher(engine, max_batch=64, max_wait_us=500)
+    got = [np.full(n, -1, dtype=np.int32) for _ in msgs]
+    errors = []
+
+    def instance(t):
+        try:
+            for i in range(t, n, 16):
+                r = reqs[i]
+                nw = (int(r["bitlen"]) + 63) // 64
+                w = words[int(r["word_offset"]):int(r["word_offset"]) + nw]
+                for k in (t % 2, 1 - t % 2):
+                    got[k][i] = b.verify(msgs[k], int(r["offset"]), int(r["bitlen"]), int(r["level_size"]), w,
+                                         sigs[64 * i:64 * i + 64])
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    ths = [threading.Thread(target=instance, args=(t,)) for t in range(16)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(120)
+    batches, requests = b.stats()
+    b.close()
+    assert not errors, errors
+    for k in range(2):
+        assert np.array_equal(got[k], want[k]), k
+    assert requests == 2 * n and batches < requests
