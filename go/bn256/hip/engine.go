@@ -452,3 +452,83 @@ func (e *Engine) loadRegistry(pks []byte) ([]int32, error) {
 	}
 	return codes, nil
 }
+
+// Packet mirrors handel.Packet (net.go:34-44) field for field, so a caller
+// converts with hip.Packet(*p).
+type Packet struct {
+	Origin        int32
+	Level         byte
+	MultiSig      []byte
+	IndividualSig []byte
+}
+
+// ParsedPacket is Handel.NewPacket's parse step for one packet (handel.go:
+// 127-152): Err is what validatePacket / parseSignatures return (nil when the
+// packet is accepted); MultiSig is the verifySignature request of the
+// multisignature, Individual the individual signature as a one-bit request of
+// the level (nil when the packet carried none).
+type ParsedPacket struct {
+	Err        error
+	MultiSig   Request
+	Individual *Request
+}
+
+// ParsePackets parses a batch of packets received by the instances
+// receivers[i] (hg_parse_packets: origin and level checks, MultiSignature /
+// WilffBitSet / willf unmarshal, bit length, empty set, individual signature
+// and IndexAtLevel, in the reference's order).
+func (e *Engine) ParsePackets(receivers []int, pkts []Packet) ([]ParsedPacket, error) {
+	n := len(pkts)
+	if len(receivers) != n {
+		return nil, &DeviceError{Code: C.HG_ERR_ARG, Msg: "ParsePackets: one receiver per packet"}
+	}
+	if n == 0 {
+		return nil, nil
+	}
+	var pool []byte
+	recs := make([]C.hg_packet, n)
+	for i, p := range pkts {
+		recs[i] = C.hg_packet{origin: C.int32_t(p.Origin), receiver: C.uint32_t(receivers[i]),
+			level: C.uint32_t(p.Level), ms_off: C.uint32_t(len(pool)), ms_len: C.uint32_t(len(p.MultiSig))}
+		pool = append(pool, p.MultiSig...)
+		if p.IndividualSig != nil {
+			recs[i].flags = C.HG_PKT_HAS_IND
+			recs[i].ind_off, recs[i].ind_len = C.uint32_t(len(pool)), C.uint32_t(len(p.IndividualSig))
+			pool = append(pool, p.IndividualSig...)
+		}
+	}
+	stride := int(C.hg_packet_stride_words(e.ctx))
+	reqs := make([]C.hg_request, 2*n)
+	words := make([]uint64, 2*n*stride)
+	sigs := make([]byte, 2*n*64)
+	codes := failedCodes(2 * n)
+	rc := C.hg_parse_packets(e.ctx, bytePtr(pool), C.size_t(len(pool)), &recs[0], C.size_t(n), C.size_t(stride),
+		&reqs[0], wordPtr(words), bytePtr(sigs), codePtr(codes))
+	if rc != C.HG_OK {
+		return nil, e.fail(rc)
+	}
+	slot := func(k int) Request {
+		r := reqs[k]
+		nw := (int(r.bitlen) + 63) / 64
+		w := make([]uint64, nw)
+		copy(w, words[int(r.word_offset):int(r.word_offset)+nw])
+		s := make([]byte, 64)
+		copy(s, sigs[64*k:64*k+64])
+		return Request{Offset: int(r.offset), LevelSize: int(r.level_size), BitLen: int(r.bitlen), Words: w, Sig: s}
+	}
+	out := make([]ParsedPacket, n)
+	buf := make([]byte, 256)
+	for i := range out {
+		if codes[i] != C.HG_OK {
+			C.hg_packet_error(e.ctx, C.int(codes[i]), &recs[i], (*C.char)(unsafe.Pointer(&buf[0])), C.size_t(len(buf)))
+			out[i].Err = errors.New(C.GoString((*C.char)(unsafe.Pointer(&buf[0]))))
+			continue
+		}
+		out[i].MultiSig = slot(i)
+		if codes[n+i] == C.HG_OK {
+			ind := slot(n + i)
+			out[i].Individual = &ind
+		}
+	}
+	return out, nil
+}

@@ -16,9 +16,9 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import partitioner as part
-from ._lib import HG_ERR_SIG_UNMARSHAL, HG_OK
+from ._lib import HG_OK
 from .engine import REQ_DTYPE, Engine
-from .sigprocessing import IncomingSig, MultiSig, bits_to_int, int_to_words
+from .sigprocessing import IncomingSig, MultiSig, int_to_words
 
 
 class BatchVerifier:
@@ -84,27 +84,40 @@ class BatchVerifier:
                 out.append(self.eng.processing_error_string(int(c)))
         return out
 
-    def verify_packets(self, packets: Sequence[Tuple[int, bytes]]) -> List[Optional[str]]:
-        """Packet-level batch: for each (level, MultiSig
-        bytes) as handel.go:390-436 receives them, MultiSignature.Unmarshal
-        (crypto.go:86-110: u16 length, WilffBitSet blob, 64-byte signature) on
-        the host, then verifySignature for every well-formed packet in one GPU
-        batch. Returns None or the error text the reference would log."""
-        out: List[Optional[str]] = [None] * len(packets)
-        todo, where = [], []
-        for i, (level, buf) in enumerate(packets):
-            try:
-                bits, sig = part.multisig_unmarshal(buf)
-            except ValueError as e:
-                out[i] = str(e)
-                continue
-            if len(sig) != 64:  # x/crypto G1.Unmarshal wants exactly 64 bytes
-                out[i] = self.eng.code_string(HG_ERR_SIG_UNMARSHAL)
-                continue
-            todo.append(IncomingSig(0, level, MultiSig(len(bits), bits_to_int(bits), sig)))
-            where.append(i)
-        for i, e in zip(where, self.verify_levels(todo) if todo else []):
-            out[i] = e
+    def verify_packets(self, packets) -> List[Optional[str]]:
+        """Handel.NewPacket -> processing -> verifySignature for packets that
+        node `node_id` received: the parse step on the GPU
+        (hg_parse_packets: validatePacket and parseSignatures, handel.go:
+        371-436), then ONE verification batch over every accepted packet's
+        multisignature. Items are packets.Packet, or (level, MultiSig bytes)
+        pairs (then sent by the first id of the level range, without an
+        individual signature). Returns None or the error text: the parse error
+        the packet is dropped with (handel.go:134-141), else verifySignature's."""
+        from .packets import Packet, pack_packets
+
+        pk = []
+        for p in packets:
+            if not isinstance(p, Packet):
+                level, buf = p
+                try:
+                    origin = part.range_level(self.node_id, self.n, level)[0]
+                except part.PartitionerError:
+                    origin = 0
+                p = Packet(origin, level, bytes(buf))
+            pk.append(p)
+        out: List[Optional[str]] = [None] * len(pk)
+        if not pk:
+            return out
+        pool, recs = pack_packets(pk, [self.node_id] * len(pk))
+        reqs, words, sigs, codes = self.eng.parse_packets(pool, recs)
+        ok = [i for i in range(len(pk)) if codes[i] == HG_OK]
+        for i in range(len(pk)):
+            if codes[i] != HG_OK:
+                out[i] = self.eng.packet_error(int(codes[i]), recs[i])
+        if ok:
+            vsigs = b"".join(sigs[64 * i:64 * i + 64] for i in ok)
+            for i, c in zip(ok, self.eng.verify_aggregate(reqs[np.array(ok)], words, vsigs)):
+                out[i] = None if c == HG_OK else self.eng.processing_error_string(int(c))
         return out
 
     def verify_ranges(self, items) -> np.ndarray:
