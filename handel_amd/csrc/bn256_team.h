@@ -139,6 +139,38 @@ HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
   fp_reduce8(r, x);
 }
 
+// acc_reduce_wide without the final conditional subtraction: the quotient
+// estimate leaves the result in [0, 2p) (the lazy rounds, bn256_xprog.h)
+HG_DEV void acc_reduce_wide_lazy(Fp& r, Acc& a) {
+#pragma unroll
+  for (int i = 0; i < kRedcSteps; i++) {
+    uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      a.c[i + j] += (uint64_t)q * p_limb(j);
+      asm("" : "+v"(a.c[i + j]));
+    }
+    a.c[i + 1] += a.c[i] >> 26;
+  }
+  uint32_t x[10];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < 10; j++) {
+    uint64_t v = a.c[kRedcSteps + j] + carry;
+    x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
+    carry = v >> 26;
+  }
+  constexpr uint32_t p9 = p_top_limb();
+  const uint32_t q = x[9] / (p9 + 1u);
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    int32_t v = (int32_t)x[i] - (int32_t)(q * p_limb(i)) + c;
+    r.l[i] = (i < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
+    c = v >> 26;
+  }
+}
+
 // conditional pieces used by the coefficient kernels
 HG_DEV void fp_sel3(Fp& r, int which, const Fp& a, const Fp& b, const Fp& c) {
 #pragma unroll

@@ -12,12 +12,15 @@
 // v_mad_u64_u32 work on LDS operands — no per-limb selects, no coefficient
 // multiplies, no carries.
 //
-// Pre-pass terms are k * x (k > 0) or k * (2p - x) (k < 0: "negated"), summed
-// limb-wise without carries: (2p)'' below is 2p with limbs in [2^26, 2^27 + 2^26)
-// (top limb 2 p_9 - 1), so (2p)''_l - x_l >= 0 for every canonical x. The
+// Pre-pass terms are k * x (k > 0) or k * (4p - x) (k < 0: "negated"), summed
+// limb-wise without carries: (4p)'' below is 4p with limbs in [2^26, 2^27 + 2^26)
+// (top limb (4p >> 234) - 1), so (4p)''_l - x_l >= 0 for every element x below
+// 2p. Elements are canonical except the results of the lazy rounds (LZ: the
+// cyclotomic squaring's, in [0, 2p); only team programs read them). The
 // generator bounds every limb sum below 2^32, every 64-bit column below 2^64
 // and the REDC result: below 2p for product-only rounds (acc_reduce: one
-// conditional subtraction), below 31p with linear terms (acc_reduce_wide).
+// conditional subtraction), below 31p with linear terms (acc_reduce_wide,
+// or its lazy form: the quotient estimate alone, [0, 2p)).
 //
 // Every table is bound to one call site: operands are absolute positions in
 // the team region (Fp12 slot s element e -> element 12 s + e, register r ->
@@ -40,7 +43,7 @@ struct XHint {
   int off, w;  // table offset and per-lane stride of the round to prefetch (off < 0: none)
 };
 struct XStream;
-template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2>
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt);
 
 
@@ -256,7 +259,7 @@ HG_DEV void x_products_ks(const Team& T, const uint32_t (&w)[W], int base, Acc& 
   }
 }
 
-template <int W, int NP, int NL, int KL, int KS>
+template <int W, int NP, int NL, int KL, int KS, int LZ = 0>
 HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst) {
   Acc acc;
   acc_zero(acc);
@@ -279,8 +282,9 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
   if constexpr (KS) x_products_ks<W, NP>(T, w, base, acc, a0, b0);
   else x_products<W, NP>(T, w, base, acc, a0, b0);
   dst = x_off(w, base + lbase + NL);
-  if constexpr (NL > 0) acc_reduce_wide(r, acc);  // linear terms: result < 31p
-  else acc_reduce(r, acc);                        // products only: < 2p, one subtraction
+  if constexpr (NL > 0 && LZ) acc_reduce_wide_lazy(r, acc);  // linear terms, lazy: [0, 2p)
+  else if constexpr (NL > 0) acc_reduce_wide(r, acc);       // linear terms: result < 31p
+  else acc_reduce(r, acc);                                  // products only: < 2p, one subtraction
 }
 
 // One round. Table layout per lane (16-bit entries): NV x (dst, NT x term),
@@ -288,7 +292,7 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 // 0), job 2 (NP2 x (u, v), NL2 x term, dst2); padded to W dwords. Both jobs
 // read before either result is stored, so in-place programs are fine.
 // off: the round's table offset
-template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2>
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   if (S.off != off) x_fetch(T, S, XHint{off, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
@@ -320,7 +324,7 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   constexpr int jbase = NV * (1 + NT);
   Fp r;
   uint32_t dst;
-  x_job<W, NP, NL, KL1, KS1>(T, w, jbase, r, dst);
+  x_job<W, NP, NL, KL1, KS1, LZ>(T, w, jbase, r, dst);
   if constexpr (NP2 > 0 || NL2 > 0) {
     Fp r2;
     uint32_t dst2;

@@ -594,17 +594,34 @@ X_SCR = 160
 P_LIMB_TOP = P >> 234
 
 
-def _p2n_limbs():
-    """(2p)'': 2p re-spread so limb l >= 2^26 (l < 9) and the top limb is 2 p_9 - 1."""
-    q = [((2 * P) >> (26 * l)) & ((1 << 26) - 1) for l in range(9)] + [(2 * P) >> 234]
+# Negations in a pre-pass or a linear term subtract x from a multiple of p
+# re-spread limb-wise, (NEG_MULT p)'' below: every limb of it dominates the
+# same limb of any element. Elements may be LAZY, below 2p instead of p: the
+# cyclotomic squaring leaves its result unreduced (LAZY_PROGRAMS), so the
+# multiple is 4p, whose top limb dominates the top limb of anything below 2p.
+NEG_MULT = 4
+
+
+def _pneg_limbs(m):
+    """(m p)'': m p re-spread so limb l >= 2^26 (l < 9) and the top limb is (m p >> 234) - 1."""
+    v = m * P
+    q = [(v >> (26 * l)) & ((1 << 26) - 1) for l in range(9)] + [v >> 234]
     out = [q[0] + (1 << 26)] + [q[l] + (1 << 26) - 1 for l in range(1, 9)] + [q[9] - 1]
-    assert sum(v << (26 * l) for l, v in enumerate(out)) == 2 * P
+    assert sum(x << (26 * l) for l, x in enumerate(out)) == v
     return out
 
 
-P2N = _p2n_limbs()
+P2N = _pneg_limbs(NEG_MULT)                          # the negation constant (HG_P2N)
 CANON_LIMB = [(1 << 26) - 1] * 9 + [P_LIMB_TOP]      # limb bounds of a canonical element
-NEG_LIMB = list(P2N)                                 # limb bounds of (2p)'' - x
+LAZY_LIMB = [(1 << 26) - 1] * 9 + [(2 * P - 1) >> 234]  # ... of an element below 2p
+NEG_LIMB = list(P2N)                                 # limb bounds of (4p)'' - x
+assert all(a <= b for a, b in zip(LAZY_LIMB, P2N)), "the negation constant must dominate every element"
+# programs whose rounds with linear terms leave their result in [0, 2p)
+# (x_round's LZ: no final conditional subtraction). Every reader of their
+# output must be a team program, which takes elements below 2p: in
+# t12_pow_v_x and team_final_exp (bn256_xprog.h, bn256_pairing.h) each
+# squaring feeds the next squaring or a MUL12, whose result is canonical.
+LAZY_PROGRAMS = ("CYC_SQR_X",)
 
 
 def _xsrc(r):
@@ -763,7 +780,7 @@ def check_xround(xr, order):
     def src_bound(code):
         if code >= X_SCR:
             return vbound[code]
-        return (P, CANON_LIMB)
+        return (2 * P, LAZY_LIMB)  # any element may be lazy (< 2p)
 
     # Every value of the pre-pass (and every lane's linear terms of a job) adds the
     # round-uniform correction K (2p)'' with K = the largest sum of negative
@@ -771,7 +788,7 @@ def check_xround(xr, order):
     vbound = {}
     for i, key in enumerate(order):
         kp = xr.kp if xr.kp >= 0 else sum(-k for _, k in key if k < 0)  # -1: per-lane correction
-        val, limbs = kp * 2 * P, [kp * x for x in P2N]
+        val, limbs = kp * NEG_MULT * P, [kp * x for x in P2N]
         for src, k in key:
             if k > 0:
                 v, lb = src_bound(src)
@@ -802,7 +819,7 @@ def check_xround(xr, order):
                 for j in range(10):
                     cols[i + j] += lu[i] * lv[j]
         if nl > 0:
-            T += kl * 2 * P * (1 << R_BITS)
+            T += kl * NEG_MULT * P * (1 << R_BITS)
             for i in range(10):
                 cols[R_BITS // 26 + i] += kl * P2N[i]
         for src, k in L["lin"]:
@@ -1218,6 +1235,7 @@ def emit_x(X, path):
              "// Two-phase team programs executed by bn256_xprog.h (encoding: see there),",
              "// one table per call-site instance (absolute team element indices).",
              "#pragma once", "#include <stdint.h>", "namespace hg {",
+             f"// HG_P2N: ({NEG_MULT}p)'' (the negation constant of pre-pass and linear terms)",
              "#define HG_P2N " + ", ".join("0x%08xu" % v for v in P2N),
              "enum XProg { " + ", ".join(f"XP_{n}" for n in X_PROGRAMS) + " };",
              f"static constexpr int kXFetchWords = {X_FETCH_WORDS};",
@@ -1241,8 +1259,10 @@ def emit_x(X, path):
         for i, (bx, off) in enumerate(rounds):
             # each round prefetches the next round's words (the last one: the caller's hint)
             nxt = f"XHint{{{rounds[i + 1][1]}, {rounds[i + 1][0].words()}}}" if i + 1 < len(rounds) else "h"
+            lz = int(name in LAZY_PROGRAMS and bx.nl > 0)
+            assert not (lz and bx.fused), "a lazy round is not fused"
             calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
-                         f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}>(T, S, {off}, {nxt});")
+                         f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
