@@ -43,7 +43,8 @@ struct XHint {
   int off, w;  // table offset and per-lane stride of the round to prefetch (off < 0: none)
 };
 struct XStream;
-template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ>
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ,
+          int EF>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt);
 
 
@@ -267,8 +268,11 @@ HG_DEV void x_products_ks(const Team& T, const uint32_t (&w)[W], int base, Acc& 
   }
 }
 
-template <int W, int NP, int NL, int KL, int KS, int LZ = 0>
-HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst) {
+// EF: a0, b0 already hold the first product's operands (read before the
+// pre-pass: plain elements, see x_round)
+template <int W, int NP, int NL, int KL, int KS, int LZ = 0, int EF = 0>
+HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst, Fp a0 = Fp{},
+                  Fp b0 = Fp{}) {
   Acc acc;
   acc_zero(acc);
   constexpr int lbase = 2 * NP;
@@ -276,8 +280,7 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
   // together, so the job pays one LDS round trip before its first mad
   Fp lx[NL > 0 ? NL : 1];
   if constexpr (NL > 0) x_for<NL>([&](auto t) { ld_fp_a8(lx[t], x_at(T, x_term_off(w, base + lbase + t))); });
-  Fp a0, b0;
-  if constexpr (NP > 0) {
+  if constexpr (NP > 0 && !EF) {
     ld_fp_a8(a0, x_at(T, x_off(w, base)));
     ld_fp_a8(b0, x_at(T, x_off(w, base + 1)));
   }
@@ -300,12 +303,22 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 // 0), job 2 (NP2 x (u, v), NL2 x term, dst2); padded to W dwords. Both jobs
 // read before either result is stored, so in-place programs are fine.
 // off: the round's table offset
-template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ>
+template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ,
+          int EF>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   if (S.off != off) x_fetch(T, S, XHint{off, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
   x_for<W>([&](auto i) { w[i] = S.w[i]; });
   if (nxt.off >= 0) x_fetch(T, S, nxt);
+  constexpr int jbase = NV * (1 + NT);
+  // EF (generator): every lane's first product reads plain elements, so its
+  // operands are read with the pre-pass's inputs and the products do not wait
+  // for the pre-pass's stores to come back
+  Fp e0, e1;
+  if constexpr (EF) {
+    ld_fp_a8(e0, x_at(T, x_off(w, jbase)));
+    ld_fp_a8(e1, x_at(T, x_off(w, jbase + 1)));
+  }
   if constexpr (NV > 0) {
     // every lane evaluates every combination (a lane without one reads the
     // ZERO register with coefficient 0: valid offsets, discarded result), and
@@ -329,10 +342,10 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     });
     team_sync();
   }
-  constexpr int jbase = NV * (1 + NT);
   Fp r;
   uint32_t dst;
-  x_job<W, NP, NL, KL1, KS1, LZ>(T, w, jbase, r, dst);
+  if constexpr (EF) x_job<W, NP, NL, KL1, KS1, LZ, EF>(T, w, jbase, r, dst, e0, e1);
+  else x_job<W, NP, NL, KL1, KS1, LZ>(T, w, jbase, r, dst);
   if constexpr (NP2 > 0 || NL2 > 0) {
     Fp r2;
     uint32_t dst2;

@@ -639,6 +639,7 @@ class XRound:
         self.nv, self.nt, self.np, self.nl, self.lanes, self.name = nv, nt, np_, nl, lanes, name
         self.np2, self.nl2 = np2, nl2
         self.ks1 = self.ks2 = 0  # Karatsuba products per job (set by check_xround)
+        self.ef = 0  # the first product's operands are plain elements (compile_round)
 
         def negk(terms):
             return sum(-k for _, k in terms if k < 0)
@@ -729,6 +730,17 @@ def compile_round(lanes, name, scratch_cap, lanes2=None):
 
     per_lane = jobs(lanes)
     per_lane2 = jobs(lanes2) if lanes2 is not None else []
+    # early first product (x_round's EF): when every lane has a product whose
+    # operands are both plain elements (no pre-pass value), it goes first and
+    # its operands are read together with the pre-pass's inputs, so the
+    # products start without waiting for a second LDS round trip
+    ef = int(lanes2 is None and any(p for _, p, _ in per_lane)
+             and all(any(u < X_SCR and v < X_SCR for u, v in p) for _, p, _ in per_lane if p))
+    if ef:
+        for i, (d, p, q) in enumerate(per_lane):
+            if p:
+                k = next(j for j, (u, v) in enumerate(p) if u < X_SCR and v < X_SCR)
+                per_lane[i] = (d, [p[k]] + p[:k] + p[k + 1:], q)
     if lanes2 is not None:
         # the first job's destinations are written after the second job reads: no overlap
         d1 = {d for d, _, _ in per_lane}
@@ -766,6 +778,7 @@ def compile_round(lanes, name, scratch_cap, lanes2=None):
             L["dst2"] = dst2
         out.append(L)
     xr = XRound(nv, nt, np_, nl, out, name, np2, nl2)
+    xr.ef = ef
     try:
         check_xround(xr, order)
     except AssertionError:
@@ -1156,6 +1169,7 @@ def bind(xr, binding, ctx):
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
     out.ks1, out.ks2 = xr.ks1, xr.ks2
+    out.ef = xr.ef
     return out
 
 
@@ -1262,7 +1276,7 @@ def emit_x(X, path):
             lz = int(name in LAZY_PROGRAMS and bx.nl > 0)
             assert not (lz and bx.fused), "a lazy round is not fused"
             calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
-                         f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}>(T, S, {off}, {nxt});")
+                         f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}, {bx.ef}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
