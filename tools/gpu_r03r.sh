@@ -13,7 +13,7 @@ timeout -k 10 500 python -u bench.py > $O/bench_$R.json 2> $O/bench_$R.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl_$R -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-extra > $O/tl_$R.log 2>&1
 rc=$?
 if [ -d $O/tl_$R ]; then
-  python3 tools/step_timeline.py $O/tl_$R/* > $O/tl_$R.txt 2>&1
+  python3 tools/step_timeline.py $O/tl_$R > $O/tl_$R.txt 2>&1
   rm -f $O/tl_$R/*/*.db $O/tl_$R/*.db
 fi
 exit $rc
