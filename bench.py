@@ -434,6 +434,12 @@ class AggregateWorkload:
     def pack(self):
         self.eng.pack_verdicts_device(self.d_codes.data_ptr(), self.n, self.d_bits.data_ptr(), self.stream.cuda_stream)
 
+    def submit_bits(self):
+        """submit + pack in one submission (hg_verify_aggregate_device_bits)."""
+        self.eng.verify_aggregate_device_bits(self.d_reqs.data_ptr(), self.n, self.d_words.data_ptr(),
+                                              self.d_sigs.data_ptr(), self.d_codes.data_ptr(), self.d_bits.data_ptr(),
+                                              self.stream.cuda_stream)
+
     def check(self, codes=None):
         got = (codes if codes is not None else self.d_codes).cpu().numpy()
         assert np.array_equal(got, self.expect), \
@@ -629,9 +635,9 @@ def main():
     gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev) for _ in range(world)]
 
     def step():
-        head.submit()
-        # verdict bitset (bit i = check i valid), gathered over RCCL: the only cross-GPU traffic
-        head.pack()
+        # the batch's verdicts and their bitset (bit i = check i valid), then
+        # the bitsets gathered over RCCL: the only cross-GPU traffic
+        head.submit_bits()
         gather_verdicts(head.d_bits.to(coll_dev), world, gathered)
 
     for _ in range(max(args.warmup, 1)):

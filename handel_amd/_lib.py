@@ -78,6 +78,7 @@ SIGNATURES = {
     "hg_pack_verdicts_device": (_I, [_P, _P, _SZ, _P, _P]),
     "hg_verify_aggregate": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P, _P]),
     "hg_verify_aggregate_device": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
+    "hg_verify_aggregate_device_bits": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
     "hg_verify_aggregate_msg": (_I, [_P, _P, _SZ, _P, _SZ, _P, _SZ, _P, _P, _P]),
     "hg_verify_multisig": (_I, [_P, _P, _P, _SZ, _P, _SZ, _P, _P]),
     "hg_aggregate_pk": (_I, [_P, _P, _SZ, _P, _SZ, _P, _P]),

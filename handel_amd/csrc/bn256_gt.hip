@@ -703,6 +703,36 @@ __global__ __launch_bounds__(64) void k_gt_compare(const Gt* fe, const Gt* y, in
   if (l == 0 && codes[r] == HG_OK) codes[r] = all ? HG_OK : HG_ERR_SIG_INVALID;
 }
 
+// k_gt_compare plus the verdict bitset (hg_pack_verdicts_device's layout: bit
+// j of byte b = request 8b + j valid), one wave per byte: the step's pack
+// launch and its dependency gap fold into the comparison
+__global__ __launch_bounds__(64) void k_gt_compare_bits(const Gt* fe, const Gt* y, int n, int32_t* codes,
+                                                        uint8_t* bits) {
+  const int b = blockIdx.x;
+  const int l = threadIdx.x;
+  uint2 a[8], v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int r = min(8 * b + j, n - 1);
+    a[j] = l < 60 ? reinterpret_cast<const uint2*>(fe[r].w)[l] : make_uint2(0, 0);
+    v[j] = l < 60 ? reinterpret_cast<const uint2*>(y[r].w)[l] : make_uint2(0, 0);
+  }
+  bool mine = false;  // lane j: request 8b + j verified
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const bool all = __ballot(a[j].x != v[j].x || a[j].y != v[j].y) == 0;
+    const int r = 8 * b + j;
+    if (l == j && r < n) {
+      int32_t c = codes[r];
+      if (c == HG_OK) c = all ? HG_OK : HG_ERR_SIG_INVALID;
+      codes[r] = c;
+      mine = c == HG_OK;
+    }
+  }
+  const uint64_t m = __ballot(mine);
+  if (l == 0) bits[b] = (uint8_t)(m & 0xffu);
+}
+
 // ------------------------------------------------------------------ launchers
 void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s) {
   if (n > 0) k_gt_keys<4><<<nblk(n, 4), 64, 0, s>>>(reg, n, tab, h, out);
@@ -739,6 +769,9 @@ void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* 
 }
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s) {
   if (n > 0) k_gt_compare<<<n, 64, 0, s>>>(fe, y, n, codes);
+}
+void launch_gt_compare_bits(const Gt* fe, const Gt* y, int n, int32_t* codes, uint8_t* bits, hipStream_t s) {
+  if (n > 0) k_gt_compare_bits<<<(n + 7) / 8, 64, 0, s>>>(fe, y, n, codes, bits);
 }
 
 }  // namespace hg

@@ -705,9 +705,12 @@ __global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t
 // pointers, on stream s; d_lvl holds the level codes and is updated in place
 // (nullptr: computed here when the flow needs them). caps: the fold's list
 // capacities (nullptr: bounded by the registry size).
+// d_bits (nullable): the verdict bitset of the codes, written in the same
+// submission (hg_pack_verdicts_device's layout)
 static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
                                    const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
-                                   bool verify, hipStream_t s, const FoldCaps* caps = nullptr) {
+                                   bool verify, hipStream_t s, const FoldCaps* caps = nullptr,
+                                   uint8_t* d_bits = nullptr) {
   if (verify && !c->has_msg) {
     c->err = "hg_set_message was not called";
     return HG_ERR_ARG;
@@ -762,7 +765,8 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
       fold.stop();
       HG_CHECK(c, hipEventRecord(c->ev_join, c->side));
       HG_CHECK(c, hipStreamWaitEvent(s, c->ev_join, 0));
-      launch_gt_compare(c->gt_fe.p, c->gt_y.p, (int)n, d_codes, s);
+      if (d_bits) launch_gt_compare_bits(c->gt_fe.p, c->gt_y.p, (int)n, d_codes, d_bits, s);
+      else launch_gt_compare(c->gt_fe.p, c->gt_y.p, (int)n, d_codes, s);
       all.stop();
       int rc = check_launch(c);
       if (rc) return rc;
@@ -778,6 +782,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     PhaseTimer t(c, HG_PHASE_VERIFY, s);
     launch_verify_sig(c->pts1.p, (int)n, c->d_lines, c->gt_y.p, d_codes, s);
     t.stop();
+    if (d_bits) launch_pack_verdicts(d_codes, (int)n, d_bits, s);
     all.stop();
     int rc = check_launch(c);
     if (rc) return rc;
@@ -812,6 +817,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
       timed_verify(c, c->checks.p, (int)n, d_codes, s);
     }
   }
+  if (d_bits) launch_pack_verdicts(d_codes, (int)n, d_bits, s);
   all.stop();
   int rc = check_launch(c);
   if (rc) return rc;
@@ -1214,6 +1220,16 @@ int hg_verify_aggregate_device(hg_ctx* c, const hg_request* d_reqs, size_t n, co
   HG_CHECK(c, hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   return aggregate_device_locked(c, d_reqs, n, d_words, d_sigs, d_codes, d_agg_pk_out, nullptr, true, s);
+}
+
+int hg_verify_aggregate_device_bits(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                                    const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_bits, void* stream) {
+  if (!c || (n && (!d_reqs || !d_sigs || !d_codes || !d_bits)) || n > (size_t)INT32_MAX) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return aggregate_device_locked(c, d_reqs, n, d_words, d_sigs, d_codes, nullptr, nullptr, true, s, nullptr, d_bits);
 }
 
 int hg_verify_aggregate(hg_ctx* c, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,

@@ -41,11 +41,13 @@ def gather_verdicts(bits: torch.Tensor, world: int, out: List[torch.Tensor] = No
     """all_gather of equal-size bitsets (every rank gets every rank's verdicts)."""
     import torch.distributed as dist
 
+    if world == 1:  # one rank: the gather is the identity
+        if out is None:
+            return [bits]
+        out[0] = bits
+        return out
     if out is None:
         out = [torch.empty_like(bits) for _ in range(world)]
-    if world == 1:
-        out[0].copy_(bits)
-        return out
     dist.all_gather(out, bits)
     return out
 

@@ -242,6 +242,13 @@ class Engine:
                                                       d_agg or None, stream or None),
                     "hg_verify_aggregate_device")
 
+    def verify_aggregate_device_bits(self, d_reqs: int, n: int, d_words: int, d_sigs: int, d_codes: int,
+                                     d_bits: int, stream: int = 0):
+        """verify_aggregate_device + the verdict bitset in one submission."""
+        self._check(self.L.hg_verify_aggregate_device_bits(self.ctx, d_reqs, n, d_words, d_sigs, d_codes, d_bits,
+                                                           stream or None),
+                    "hg_verify_aggregate_device_bits")
+
     def aggregate_pk(self, reqs: np.ndarray, words: np.ndarray) -> Tuple[bytes, np.ndarray]:
         reqs = np.ascontiguousarray(reqs, dtype=REQ_DTYPE)
         words = np.ascontiguousarray(words, dtype=np.uint64)

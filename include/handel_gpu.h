@@ -202,6 +202,13 @@ size_t hg_registry_non_g2(hg_ctx* ctx);
 int hg_verify_aggregate_device(hg_ctx* ctx, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
                                const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg_pk_out, void* stream);
 
+/* hg_verify_aggregate_device (verdicts only) plus the verdict bitset of the
+ * codes (hg_pack_verdicts_device's layout, ceil(n/8) bytes) in the same
+ * submission: the serving step's codes -> bitset launch folds into the
+ * comparison (processing.go:270-287's err == nil branch, batched). */
+int hg_verify_aggregate_device_bits(hg_ctx* ctx, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                                    const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_bits, void* stream);
+
 /* Batched PublicKey.Combine fold only: n requests -> n*128 B aggregate keys
  * (bn256/go/bn256.go:97-105). codes: HG_OK, HG_ERR_LEVEL or HG_ERR_EMPTY_AGG. */
 int hg_aggregate_pk(hg_ctx* ctx, const hg_request* reqs, size_t n, const uint64_t* words, size_t nwords,

@@ -397,3 +397,41 @@ print(json.dumps({"ok": ok, "levels": levels}))
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["ok"] == [True] * 6
     assert out["levels"] == [0, 0, 0, 1, 1, 1]
+
+
+@pytest.mark.parametrize("level,overlap", [(2, 1), (2, 0), (0, 1)], ids=["gt-overlap", "gt-serial", "g2fold"])
+def test_fused_bitset_matches_pack(level, overlap):
+    """hg_verify_aggregate_device_bits: the codes are the plain call's and the
+    bitset is hg_pack_verdicts_device's, on a batch whose size is not a
+    multiple of 8 (the tail byte), through the fused compare (GT path beside
+    the fold), the serial GT path and the G2 fold (pack after the check)."""
+    import torch
+
+    import bench
+    from handel_amd.engine import Engine
+
+    e = Engine(device=0, flavor="go")
+    try:
+        assert e.set_message(bench.LIB_MESSAGE) == 0
+        n = 1001
+        reqs, words, sigs, expect, _, _ = bench.make_aggregate_batch(e, 700, n, seed=77)
+        e.set_aggregate_level(level)
+        e.set_fold_overlap(overlap)
+        dev = torch.device("cuda", 0)
+        d_reqs = torch.from_numpy(reqs.view(np.uint8).copy()).to(dev)
+        d_words = torch.from_numpy(words.view(np.int64).copy()).to(dev)
+        d_sigs = torch.from_numpy(np.frombuffer(sigs, dtype=np.uint8).copy()).to(dev)
+        codes = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        bits = torch.full(((n + 7) // 8,), 0xAA, dtype=torch.uint8, device=dev)
+        ref = torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        for _ in range(2):  # the second submission reuses every workspace
+            e.verify_aggregate_device_bits(d_reqs.data_ptr(), n, d_words.data_ptr(), d_sigs.data_ptr(),
+                                           codes.data_ptr(), bits.data_ptr(), s)
+        e.pack_verdicts_device(codes.data_ptr(), n, ref.data_ptr(), s)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(codes.cpu().numpy(), expect)
+        assert torch.equal(bits, ref)
+        assert e.aggregate_tables() == level
+    finally:
+        e.close()

@@ -33,7 +33,8 @@ def main():
     variants = {
         "submit": lambda: head.submit(),
         "submit+pack": lambda: (head.submit(), head.pack()),
-        "submit+pack+gather": lambda: (head.submit(), head.pack(), gather_verdicts(head.d_bits, 1, gathered)),
+        "submit_bits": lambda: head.submit_bits(),
+        "submit_bits+gather": lambda: (head.submit_bits(), gather_verdicts(head.d_bits, 1, gathered)),
     }
     out = {}
     for name, fn in variants.items():
