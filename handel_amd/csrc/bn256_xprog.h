@@ -134,30 +134,22 @@ HG_DEV void x_lincomb(const Team& T, const uint32_t (&w)[W], int base, uint32_t 
   for (int l = 0; l < 10; l++) out[l] = K >= 0 ? acc[l] : acc[l] + negk * kP2N[l];
 }
 
-// x_lincomb on operands already loaded (xs[t] = the element of term t).
-// Each term and limb is ONE v_mad_u64_u32 into a 64-bit accumulator (the
-// empty asm keeps the 64-bit result live, so LLVM does not narrow it back to
-// a 32-bit multiply plus an add); only the low 32 bits are used: the
-// generator keeps every limb sum below 2^32, and a negative coefficient's
-// 2^32 wrap cancels in them.
+// x_lincomb on operands already loaded (xs[t] = the element of term t)
 template <int W, int NT, int K>
 HG_DEV void x_lincomb_sum(const uint32_t (&w)[W], int base, const Fp (&xs)[NT], uint32_t (&out)[10]) {
-  uint64_t acc[10];
+  uint32_t acc[10];
 #pragma unroll
-  for (int l = 0; l < 10; l++) acc[l] = K >= 0 ? (uint64_t)((uint32_t)K * kP2N[l]) : 0u;
+  for (int l = 0; l < 10; l++) acc[l] = K >= 0 ? (uint32_t)K * kP2N[l] : 0u;
   uint32_t negk = 0;
 #pragma unroll
   for (int t = 0; t < NT; t++) {
     const int32_t c = x_coef(w, base + t);
     if constexpr (K < 0) negk += c < 0 ? (uint32_t)-c : 0u;
 #pragma unroll
-    for (int l = 0; l < 10; l++) {
-      acc[l] += (uint64_t)(uint32_t)c * xs[t].l[l];
-      asm("" : "+v"(acc[l]));
-    }
+    for (int l = 0; l < 10; l++) acc[l] += (uint32_t)c * xs[t].l[l];
   }
 #pragma unroll
-  for (int l = 0; l < 10; l++) out[l] = K >= 0 ? (uint32_t)acc[l] : (uint32_t)acc[l] + negk * kP2N[l];
+  for (int l = 0; l < 10; l++) out[l] = K >= 0 ? acc[l] : acc[l] + negk * kP2N[l];
 }
 
 // One job: sum of NP products of LDS operands plus NL R-shifted linear terms,
