@@ -591,8 +591,8 @@ def roofline(fpmul: int, ms: float, kernel: str, traffic_pattern: str, work: str
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--committees", action="store_true",
                     help="config 5: each rank is one committee of 4096 signers (own 4096-key registry)")
