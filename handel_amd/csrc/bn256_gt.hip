@@ -665,6 +665,10 @@ template <int TEAMS, bool kStore>
 __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const uint8_t* sig_bytes, int flavor, int n,
                                                    const LineCoef* tab, const Gt* y, Gt* fe, int32_t* codes) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kSigTeamWords];
+  // kStore runs beside the GT fold on another stream, whose waves share the
+  // SIMDs: the pairing wave (the step's critical path) wins the issue
+  // arbitration, the fold's waves take the cycles it leaves
+  if (kStore) __builtin_amdgcn_s_setprio(3);
   Team T = make_team(lds, kSigTeamWords);
   uint32_t* F = team_regs(T);
   const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
