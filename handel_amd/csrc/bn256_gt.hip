@@ -549,41 +549,37 @@ __global__ __launch_bounds__(64) void k_gt_combine(int n, const GtHdr* hdr, cons
 // f = Miller(G2Base at -sig) (x/crypto optate.go miller with the G2Base lines
 // from the table): per doubling f^2 with the line's evaluation at -sig beside
 // it (SDBL), then f * line; an addition's line is evaluated beside the
-// previous product (LFEV). Lanes 12..15 evaluate, lanes 0..11 run the Fp12
+// previous product (LFEVN). Lanes 12..15 evaluate, lanes 0..11 run the Fp12
 // job, so the evaluation is free.
+//
+// The table's lines are normalised (k_g2_lines: c' + b' w + w^3), so f * line
+// is 4 products per lane plus the w^3 shift as a linear term.
 using ISdbl = XInst<XP_SDBL, S_F, S_F>;
 using ILfev = XInst<XP_LFEV, S_F, S_F>;
 using IFeval = XInst<XP_FEVAL>;
 using ILfix = XInst<XP_LINE_FIX, S_F, S_F>;
 
 // The G2Base lines reach the team's registers through one VGPR element per
-// lane (lane tl < 6 holds Fp tl of a line: a.x, a.y, bx.x, bx.y, cy.x, cy.y),
-// read from the table one publication ahead, so the L2 latency of the read
-// overlaps the rounds between (it used to be exposed twice per Miller step).
+// lane (lane tl < 4 holds Fp tl of a line: bx.x, bx.y, cy.x, cy.y), read from
+// the table one publication ahead, so the L2 latency of the read overlaps the
+// rounds between.
 struct LinePipe {
   Fp c;
 };
-// fetch the part of line s that lanes [lo, hi) publish next
-HG_DEV void line_fetch(const Team& T, LinePipe& P, const LineCoef* tab, int s, int lo, int hi) {
-  if (T.tl >= lo && T.tl < hi) P.c = reinterpret_cast<const Fp*>(&tab[s])[T.tl];
+HG_DEV void line_fetch(const Team& T, LinePipe& P, const LineCoef* tab, int s) {
+  if (T.tl < 4) P.c = reinterpret_cast<const Fp*>(&tab[s])[T.tl];
 }
 // FBX, FCY of the held line (the evaluation's inputs), then the next line's
-// FBX, FCY into flight; FA likewise
-HG_DEV void publish_line_bc(const Team& T, uint32_t* F, LinePipe& P, const LineCoef* tab, int next) {
-  if (T.tl >= 2 && T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, P.c);
+// into flight
+HG_DEV void publish_line(const Team& T, uint32_t* F, LinePipe& P, const LineCoef* tab, int next) {
+  if (T.tl < 4) st_fp(F + (R_FBX_x + T.tl) * 10, P.c);
   team_sync();
-  if (next < kNumLines) line_fetch(T, P, tab, next, 2, 6);
-}
-HG_DEV void publish_line_a(const Team& T, uint32_t* F, LinePipe& P, const LineCoef* tab, int next) {
-  if (T.tl < 2) st_fp(F + (R_FA_x + T.tl) * 10, P.c);
-  team_sync();
-  if (next < kNumLines) line_fetch(T, P, tab, next, 0, 2);
-}
-HG_DEV void sig_unit_fix(const Team& T, uint32_t* F, bool use_s) {
-  team_sync();
-  unit_line_regs(T, F, !use_s, R_FA_x, R_FB_x, R_FC_x);
+  if (next < kNumLines) line_fetch(T, P, tab, next);
 }
 
+// A signature at infinity contributes e(inf, G2Base) = 1: with SX = NSY = 0
+// every evaluated line is w^3, an element of Fp4 the final exponentiation maps
+// to 1, so f needs no unit-line substitution.
 HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& sy, bool use_s,
                             const LineCoef* tab, XStream& S, XHint after) {
   const int8_t naf[kNafLen] = HG_NAF;
@@ -595,27 +591,23 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
     fp_neg(nsy, sy);
     st_fp(F + R_ZERO * 10, zero);
     st_fp(F + R_ONE * 10, one);
-    st_fp(F + R_SX * 10, sx);
-    st_fp(F + R_NSY * 10, nsy);
+    st_fp(F + R_SX * 10, use_s ? sx : zero);
+    st_fp(F + R_NSY * 10, use_s ? nsy : zero);
   }
   team_sync();
   LinePipe P;
   fp_zero(P.c);
-  line_fetch(T, P, tab, 0, 0, 6);
+  line_fetch(T, P, tab, 0);
   int s = 0;
   for (int i = kNafLen - 1; i > 0; i--) {
     const int d = naf[i - 1];
-    publish_line_bc(T, F, P, tab, s + 1);
-    publish_line_a(T, F, P, tab, s + 1);
+    publish_line(T, F, P, tab, s + 1);
     // f^2 (f = 1 on the first digit) beside line s evaluated at -sig
     ISdbl::run(T, S, d != 0 ? xh<ILfev>() : xh<ILfix>());
-    sig_unit_fix(T, F, use_s);
     const XHint after_digit = i > 1 ? xh<ISdbl>() : xh<IFeval>();
     if (d != 0) {
-      publish_line_bc(T, F, P, tab, s + 2);  // read by the evaluation beside f * line s
+      publish_line(T, F, P, tab, s + 2);  // read by the evaluation beside f * line s
       ILfev::run(T, S, xh<ILfix>());
-      publish_line_a(T, F, P, tab, s + 2);
-      sig_unit_fix(T, F, use_s);
       ILfix::run(T, S, after_digit);
       s += 2;
     } else {
@@ -624,14 +616,10 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
     }
   }
   // the two Frobenius lines
-  publish_line_bc(T, F, P, tab, s + 1);
-  publish_line_a(T, F, P, tab, s + 1);
+  publish_line(T, F, P, tab, s + 1);
   IFeval::run(T, S, xh<ILfev>());
-  sig_unit_fix(T, F, use_s);
-  publish_line_bc(T, F, P, tab, kNumLines);
+  publish_line(T, F, P, tab, kNumLines);
   ILfev::run(T, S, xh<ILfix>());
-  publish_line_a(T, F, P, tab, kNumLines);
-  sig_unit_fix(T, F, use_s);
   ILfix::run(T, S, after);
 }
 

@@ -24,9 +24,11 @@ struct CheckIn {
   PointG2 pk;
   PointG1 sig;
 };
-// A G2Base Miller-loop line: value c + b w + a w^3 with b = bx * Px, c = cy * Py
+// A G2Base Miller-loop line, normalised: x/crypto's line c + b w + a w^3
+// divided by its constant coefficient a (an Fp2 factor, removed by the final
+// exponentiation), i.e. c' + b' w + w^3 with b' = bx * Px, c' = cy * Py
 struct LineCoef {
-  Fp2 a, bx, cy;
+  Fp2 bx, cy;
 };
 static constexpr int kNumLines = 65 + 18 + 2;  // doublings + NAF additions + 2 Frobenius lines
 

@@ -243,6 +243,16 @@ __global__ __launch_bounds__(64) void k_hash_point(const uint32_t* k_words, Poin
 // ------------------------------------------------------------------ fixed G2Base lines
 // Same step order as the Miller loop in k_verify: for i = 65..1 a doubling
 // line, then an addition line when NAF[i-1] != 0, then the two Frobenius lines.
+// Each line is stored divided by its constant coefficient a (LineCoef): the
+// line products then take 4 Fp products per lane instead of 6 (the w^3 term
+// is a coefficient shift), and the Fp2 factors are removed by the final
+// exponentiation. No G2Base line has a = 0 (tests/test_oracle.py).
+HG_DEV void put_line(LineCoef& out, const Fp2& a, const Fp2& bx, const Fp2& cy) {
+  Fp2 ai;
+  f2_inv(ai, a);
+  f2_mul(out.bx, bx, ai);
+  f2_mul(out.cy, cy, ai);
+}
 __global__ __launch_bounds__(64) void k_g2_lines(LineCoef* tab) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int8_t naf[kNafLen] = HG_NAF;
@@ -254,17 +264,17 @@ __global__ __launch_bounds__(64) void k_g2_lines(LineCoef* tab) {
   R.y = qy;
   f2_one(R.z);
   f2_one(R.t);
-  Fp2 r2, nqy;
+  Fp2 r2, nqy, a, bx, cy;
   f2_sqr(r2, qy);
   f2_neg(nqy, qy);
   int s = 0;
   for (int i = kNafLen - 1; i > 0; i--) {
-    line_double(tab[s].a, tab[s].bx, tab[s].cy, R);
-    s++;
+    line_double(a, bx, cy, R);
+    put_line(tab[s++], a, bx, cy);
     int d = naf[i - 1];
     if (d != 0) {
-      line_add(tab[s].a, tab[s].bx, tab[s].cy, R, qx, d > 0 ? qy : nqy, r2);
-      s++;
+      line_add(a, bx, cy, R, qx, d > 0 ? qy : nqy, r2);
+      put_line(tab[s++], a, bx, cy);
     }
   }
   Fp2 q1x, q1y, t;
@@ -273,12 +283,13 @@ __global__ __launch_bounds__(64) void k_g2_lines(LineCoef* tab) {
   f2_conj(t, qy);
   f2_mul(q1y, t, g1[3]);
   f2_sqr(r2, q1y);
-  line_add(tab[s].a, tab[s].bx, tab[s].cy, R, q1x, q1y, r2);
-  s++;
+  line_add(a, bx, cy, R, q1x, q1y, r2);
+  put_line(tab[s++], a, bx, cy);
   Fp2 q2x;
   f2_muls(q2x, qx, g2[2]);
   f2_sqr(r2, qy);
-  line_add(tab[s].a, tab[s].bx, tab[s].cy, R, q2x, qy, r2);
+  line_add(a, bx, cy, R, q2x, qy, r2);
+  put_line(tab[s], a, bx, cy);
 }
 
 // ------------------------------------------------------------------ aggregation

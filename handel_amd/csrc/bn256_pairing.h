@@ -101,8 +101,11 @@ struct CheckCtx {
 
 // Writes the team's G2 register file: point R = Q (projective, see below), Q, -Qy, the
 // Frobenius images q1 = pi(Q), -q2 = (Qx gamma2[2], Qy) (optate.go miller),
-// the G1 points and constants.
-HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
+// the G1 points and constants. has_fixed && C.use_s: the G2Base pairing at
+// -sig contributes; otherwise SX = NSY = 0 make every evaluated G2Base line
+// w^3, an element of Fp4 that the final exponentiation maps to 1 (x/crypto's
+// GT = 1 for an infinity input).
+HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed) {
   const Fp2 g1[6] = HG_GAMMA1;
   const Fp g2[6] = HG_GAMMA2;
   Fp2 nqy, q1x, q1y, q2x, t, one2;
@@ -126,8 +129,9 @@ HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
     st_fp(F + R_ONE * 10, one);
     st_fp(F + R_PX * 10, C.hx);
     st_fp(F + R_PY * 10, C.hy);
-    st_fp(F + R_SX * 10, C.sx);
-    st_fp(F + R_NSY * 10, nsy);
+    const bool fix = has_fixed && C.use_s;
+    st_fp(F + R_SX * 10, fix ? C.sx : zero);
+    st_fp(F + R_NSY * 10, fix ? nsy : zero);
     // R = (xi Qx : xi Qy : xi) in the projective programs' coordinates, whose
     // Z register holds W = Z / xi = 1 (gen_g2_schedule.py prog_double_proj)
     Fp2 xqx, xqy;
@@ -146,25 +150,23 @@ HG_DEV void g2_regs_init(const Team& T, uint32_t* F, const CheckCtx& C) {
   team_sync();
 }
 
-// The G2Base line (a, bx, cy: 6 Fp) goes into FA, FBX, FCY from one VGPR
-// element per lane (lane tl < 6 holds Fp tl), read from the table one line
-// ahead so the L2 latency of the read overlaps the step's rounds.
+// The normalised G2Base line (bx, cy: 4 Fp; a = 1, k_g2_lines) goes into FBX,
+// FCY from one VGPR element per lane (lane tl < 4 holds Fp tl), read from the
+// table one line ahead so the L2 latency of the read overlaps the step's rounds.
 HG_DEV void fixed_line_fetch(const Team& T, Fp& held, const LineCoef* tab, int s) {
-  if (T.tl < 6 && s < kNumLines) held = reinterpret_cast<const Fp*>(&tab[s])[T.tl];
+  if (T.tl < 4 && s < kNumLines) held = reinterpret_cast<const Fp*>(&tab[s])[T.tl];
 }
 // publishes the held line, then fetches line `next`
 HG_DEV void load_fixed_line(const Team& T, uint32_t* F, Fp& held, const LineCoef* tab, int next) {
-  if (T.tl < 6) st_fp(F + (R_FA_x + T.tl) * 10, held);
+  if (T.tl < 4) st_fp(F + (R_FBX_x + T.tl) * 10, held);
   team_sync();
   fixed_line_fetch(T, held, tab, next);
 }
 
-// A point at infinity contributes the unit line (a = b = 0, c = 1). The
-// G2Base line (FA, FB, FC; FB and FC are evaluated at -sig by the step's first
-// round) is replaced before the round that multiplies it in, the pk line
-// (LA, LB, LC) before x_line_pk; each branch is taken only when some team of
-// the wave needs it. Without a fixed pairing (k_pair) the G2Base line is
-// always the unit line.
+// A pk at infinity contributes the unit line (a = b = 0, c = 1): the pk line
+// (LA, LB, LC) is replaced before x_line_pk; the branch is taken only when
+// some team of the wave needs it. The G2Base side needs no replacement
+// (g2_regs_init).
 HG_DEV void unit_line_regs(const Team& T, uint32_t* F, bool fix, int ra, int rb, int rc) {
   if (__ballot(fix) == 0) return;  // wave-uniform
   Fp z, o;
@@ -178,9 +180,6 @@ HG_DEV void unit_line_regs(const Team& T, uint32_t* F, bool fix, int ra, int rb,
     st_fp(F + r * 10, v);
   }
   team_sync();
-}
-HG_DEV void unit_line_fix(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed) {
-  unit_line_regs(T, F, !has_fixed || !C.use_s, R_FA_x, R_FB_x, R_FC_x);
 }
 HG_DEV void unit_line_pk(const Team& T, uint32_t* F, const CheckCtx& C) {
   unit_line_regs(T, F, !C.use_q, R_LA_x, R_LB_x, R_LC_x);
@@ -204,9 +203,8 @@ using AddF1 = AddStep<XP_PADD_F1_1, XP_MADD_F1_2, XP_PADD_F1_3>;
 using AddF2 = AddStep<XP_PADD_F2_1, XP_MADD_F2_2, XP_PADD_F2_3>;
 
 template <class A>
-HG_DEV void add_step(const Team& T, uint32_t* F, const CheckCtx& C, bool has_fixed, XStream& S, XHint next) {
+HG_DEV void add_step(const Team& T, uint32_t* F, const CheckCtx& C, XStream& S, XHint next) {
   A::I1::run(T, S, xh<typename A::I2>());
-  unit_line_fix(T, F, C, has_fixed);
   A::I2::run(T, S, xh<typename A::I3>());
   A::I3::run(T, S, xh<ILinePk<S_F, S_F>>());
   unit_line_pk(T, F, C);
@@ -221,7 +219,7 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   const int8_t naf[kNafLen] = HG_NAF;
   constexpr XHint kLinePk = xh<ILinePk<S_F, S_F>>();
   t12_set_one(T, S_F);
-  g2_regs_init(T, F, C);
+  g2_regs_init(T, F, C, has_fixed);
   Fp held;
   fp_zero(held);
   fixed_line_fetch(T, held, tab, 0);
@@ -233,7 +231,6 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
     if (i == kNafLen - 1) XInst<XP_PDBL_1>::run(T, S, xh<IMdbl2>());  // f = 1: no squaring
     else IMdbl1::run(T, S, xh<IMdbl2>());
     DIAG_ADD(1);
-    unit_line_fix(T, F, C, has_fixed);
     IMdbl2::run(T, S, kLinePk);
     unit_line_pk(T, F, C);
     DIAG_ADD(2);
@@ -244,15 +241,15 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
     if (d != 0) {
       load_fixed_line(T, F, held, tab, ++s);
       DIAG_ADD(0);
-      if (d > 0) add_step<AddPos>(T, F, C, has_fixed, S, step);
-      else add_step<AddNeg>(T, F, C, has_fixed, S, step);
+      if (d > 0) add_step<AddPos>(T, F, C, S, step);
+      else add_step<AddNeg>(T, F, C, S, step);
       DIAG_ADD(4);
     }
   }
   load_fixed_line(T, F, held, tab, ++s);
-  add_step<AddF1>(T, F, C, has_fixed, S, xh<AddF2::I1>());
+  add_step<AddF1>(T, F, C, S, xh<AddF2::I1>());
   load_fixed_line(T, F, held, tab, ++s);
-  add_step<AddF2>(T, F, C, has_fixed, S, after);
+  add_step<AddF2>(T, F, C, S, after);
 }
 
 HG_DEV uint32_t* team_regs(const Team& T) { return T.base + kSlots * kFp12Words; }

@@ -62,6 +62,56 @@ def test_pairing_independent_of_addition_chain():
     assert a == b
 
 
+def _g2base_lines_normalised(p, unit=False):
+    """The G2Base Miller loop of O.miller with every line divided by its
+    constant coefficient a (k_g2_lines' table, the LINE_FIX / LFEV programs):
+    yields (a, line) per step; unit: the signature at infinity (SX = NSY = 0,
+    every line w^3)."""
+    def norm(a, b, c):
+        ai = O.f2_inv(a)
+        b, c = O.f2_mul(b, ai), O.f2_mul(c, ai)
+        return a, ((O.F2_ZERO, O.F2_ZERO) if unit else (b, c))
+
+    q = O.G2_GEN
+    px, py = p
+    r, r2, nq = (q[0], q[1], O.F2_ONE, O.F2_ONE), O.f2_sqr(q[1]), (q[0], O.f2_neg(q[1]))
+    naf = O.SIX_U_PLUS_2_NAF
+    out = []
+    for i in range(len(naf) - 1, 0, -1):
+        a, b, c, r = O._line_double(r, px, py)
+        out.append(("dbl", norm(a, b, c)))
+        if naf[i - 1]:
+            a, b, c, r = O._line_add(r, q if naf[i - 1] > 0 else nq, px, py, r2)
+            out.append(("add", norm(a, b, c)))
+    q1 = (O.f2_mul(O.f2_conj(q[0]), O.XI_TO_P_MINUS_1_OVER_3), O.f2_mul(O.f2_conj(q[1]), O.XI_TO_P_MINUS_1_OVER_2))
+    mq2 = (O.f2_muls(q[0], O.XI_TO_PSQ_MINUS_1_OVER_3), q[1])
+    for pt in (q1, mq2):
+        a, b, c, r = O._line_add(r, pt, px, py, O.f2_sqr(pt[1]))
+        out.append(("add", norm(a, b, c)))
+    return out
+
+
+def _miller_normalised(p, unit=False):
+    f, first = O.F12_ONE, True
+    for kind, (a, (b, c)) in _g2base_lines_normalised(p, unit):
+        assert a != O.F2_ZERO  # the normalisation divides by every line's a
+        if kind == "dbl" and not first:
+            f = O.f12_sqr(f)
+        first = False
+        f = O._mul_line(f, O.F2_ONE, b, c)
+    return f
+
+
+def test_normalised_g2base_lines_give_the_same_pairing():
+    """The kernels' G2Base lines (a = 1): same reduced pairing at -sig as
+    x/crypto's, and the all-w^3 lines of a signature at infinity reduce to 1."""
+    assert len(_g2base_lines_normalised(O.G1_GEN)) == 85  # kNumLines
+    for k in (1, 77):
+        p = O.g1_neg(O.g1_mul(O.G1_GEN, k))
+        assert O.final_exponentiation(_miller_normalised(p)) == O.pair(p, O.G2_GEN)
+    assert O.final_exponentiation(_miller_normalised(O.G1_GEN, unit=True)) == O.F12_ONE
+
+
 def test_bilinearity_and_nondegeneracy():
     e = O.pair(O.G1_GEN, O.G2_GEN)
     assert not O.f12_is_one(e)

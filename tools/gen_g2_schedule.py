@@ -45,10 +45,10 @@ NONE = 255
 # ------------------------------------------------------------------ register file
 FP_SCALARS = ["ZERO", "ONE", "PX", "PY", "SX", "NSY"]
 # The kernels' register file (kG2Regs): the projective Miller-loop programs'
-# point, pk, line coefficients and temporaries. FA, FBX, FCY must stay
-# consecutive (load_fixed_line).
+# point, pk, line coefficients and temporaries. FBX, FCY must stay
+# consecutive (load_fixed_line: the normalised G2Base line, a = 1).
 FP2_RUNTIME = ["X", "Y", "Z", "QX", "QY", "NQY", "P1X", "P1Y", "P2X",
-               "FA", "FBX", "FCY", "FB", "FC", "LA", "LB", "LC",
+               "FBX", "FCY", "FB", "FC", "LA", "LB", "LC",
                # projective doubling temporaries
                "A", "B", "S", "C", "G",
                # projective addition temporaries
@@ -461,6 +461,36 @@ def prog_line(la, lb, lc):
     return [lanes]
 
 
+def prog_line_n(lb, lc):
+    """dst = A * (lc + lb w + w^3): a G2Base line divided by its constant
+    coefficient a (bn256_kernels.hip k_g2_lines; the Fp2 factor a is removed by
+    the final exponentiation), so the w^3 part is A * w^3, a linear term (a
+    coefficient shift, xi on the wrapped ones): 4 products per lane instead of
+    prog_line's 6."""
+    lanes = []
+    for k in range(6):
+        for c in "xy":
+            slots = []
+            for jpos, L in ((0, lc), (1, lb)):
+                i = k - jpos
+                lx, ly = [(comp(L, "x"), 1)], [(comp(L, "y"), 1)]
+                if i < 0:
+                    i += 6
+                    lx, ly = xi_lc(lx, ly)
+                fx, fy = [(comp(f"A{i}", "x"), 1)], [(comp(f"A{i}", "y"), 1)]
+                if c == "x":
+                    slots += [(fx, ly), (fy, lx)]
+                else:
+                    slots += [(fy, ly), (fx, neg(lx))]
+            i = k - 3
+            fx, fy = [(comp(f"A{i % 6}", "x"), 1)], [(comp(f"A{i % 6}", "y"), 1)]
+            if i < 0:
+                fx, fy = xi_lc(fx, fy)   # xi * A_{k+3}
+            slots.append((fx if c == "x" else fy, one()))
+            lanes.append(Lane(comp(f"D{k}", c), slots))
+    return [lanes]
+
+
 PROGRAMS = {
     "DBL": prog_double(),
     "ADD_POS": prog_add("QX", "QY", "R2"),
@@ -471,7 +501,7 @@ PROGRAMS = {
     "SQR12": prog_sqr12(),
     "MUL12": prog_mul12(),
     "LINE_PK": prog_line("LA", "LB", "LC"),
-    "LINE_FIX": prog_line("FA", "FB", "FC"),
+    "LINE_FIX": prog_line_n("FB", "FC"),
     "CYC_SQR_X": prog_cyc_sqr_x(),
     "PDBL": prog_double_proj(),
     "PADD_POS": prog_add_proj("QX", "QY"),
@@ -479,12 +509,13 @@ PROGRAMS = {
     "PADD_F1": prog_add_proj("P1X", "P1Y"),
     "PADD_F2": prog_add_proj("P2X", "QY"),
 }
+# The G2Base lines are normalised (a = 1): LINE_FIX = prog_line_n.
 # Sig-only Miller loop (bn256_gt.hip k_verify_sig): the G2Base line at -sig is
 # evaluated on lanes 12..15 beside f^2 (SDBL) or beside f * the previous line
 # (LFEV), rounds whose Fp12 jobs leave those lanes idle anyway; FEVAL alone.
 PROGRAMS["FEVAL"] = [fixed_line_eval()]
 PROGRAMS["SDBL"] = [prog_sqr12()[0] + fixed_line_eval()]
-PROGRAMS["LFEV"] = [prog_line("FA", "FB", "FC")[0] + fixed_line_eval()]
+PROGRAMS["LFEV"] = [prog_line_n("FB", "FC")[0] + fixed_line_eval()]
 # Fp12 product in the compact GT-fold team layout (context FOLD below)
 PROGRAMS["MUL12F"] = prog_mul12()
 # programs also emitted in the single-phase table format (bn256_g2sched.h)
@@ -1007,13 +1038,12 @@ def validate_x(seed=2):
         # fused Miller-loop programs: f^2 and the G2Base line beside the G2 step rounds
         f0 = [(rng.randrange(P), rng.randrange(P)) for _ in range(6)]
         flat0 = [z for pair in f0 for z in pair]
-        fl_a, fl_bx, fl_cy = (rng.randrange(P), rng.randrange(P)), (rng.randrange(P), rng.randrange(P)), \
-            (rng.randrange(P), rng.randrange(P))
+        # a normalised G2Base line (a = 1, k_g2_lines): c + b w + w^3
+        fl_bx, fl_cy = (rng.randrange(P), rng.randrange(P)), (rng.randrange(P), rng.randrange(P))
         F[REG["SX"]], F[REG["NSY"]] = rng.randrange(P), rng.randrange(P)
-        put(F, "FA", fl_a)
         put(F, "FBX", fl_bx)
         put(F, "FCY", fl_cy)
-        fix = (fl_a, O.f2_mul(fl_bx, (0, F[REG["SX"]])), O.f2_mul(fl_cy, (0, F[REG["NSY"]])))
+        fix = (O.F2_ONE, O.f2_mul(fl_bx, (0, F[REG["SX"]])), O.f2_mul(fl_cy, (0, F[REG["NSY"]])))
         unfl = lambda D: [(D[2 * k], D[2 * k + 1]) for k in range(6)]  # noqa: E731
         G = dict(F)
         sq = run_xprogram(X["MDBL_1"], G, flat0)
@@ -1070,12 +1100,13 @@ def validate_x(seed=2):
         assert unflat(run_xprogram(X["MUL12F"], dict(F), flat(f), flat(g))) == O.f12_mul(f, g), "xMUL12F"
         G = dict(F)
         la, lb, lc = [(rng.randrange(P), rng.randrange(P)) for _ in range(3)]
-        for regs in (("LA", "LB", "LC", "LINE_PK"), ("FA", "FB", "FC", "LINE_FIX")):
-            put(G, regs[0], la)
-            put(G, regs[1], lb)
-            put(G, regs[2], lc)
-            want = O._mul_line(f, la, lb, lc)
-            assert unflat(run_xprogram(X[regs[3]], G, flat(f))) == want, "x" + regs[3]
+        put(G, "LA", la)
+        put(G, "LB", lb)
+        put(G, "LC", lc)
+        assert unflat(run_xprogram(X["LINE_PK"], G, flat(f))) == O._mul_line(f, la, lb, lc), "xLINE_PK"
+        put(G, "FB", lb)
+        put(G, "FC", lc)
+        assert unflat(run_xprogram(X["LINE_FIX"], G, flat(f))) == O._mul_line(f, O.F2_ONE, lb, lc), "xLINE_FIX"
     return X
 
 
