@@ -41,13 +41,18 @@ def up_to_date(lib: str = LIB) -> bool:
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def build_library(force: bool = False, verbose: bool = True, diag: bool = False) -> str:
+def build_library(force: bool = False, verbose: bool = True, diag: bool = False, variant: str = "",
+                  defs: tuple = ()) -> str:
+    """variant: an A/B build (tools/ab_variants.sh) with extra -D defs, written
+    to _build/variants/libhandel_gpu_<variant>.so; never loaded by default."""
     lib = DIAG_LIB if diag else LIB
-    if not force and up_to_date(lib):
+    if variant:
+        lib = os.path.join(OUT_DIR, "variants", f"libhandel_gpu_{variant}.so")
+    if not force and not variant and up_to_date(lib):
         return lib
-    os.makedirs(OUT_DIR, exist_ok=True)
-    suffix = "_diag" if diag else ""
-    extra = ["-DHG_DIAG=1"] if diag else []
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    suffix = "_diag" if diag else (f"_{variant}" if variant else "")
+    extra = (["-DHG_DIAG=1"] if diag else []) + [f"-D{d}" for d in defs]
 
     def compile_one(src):
         obj = os.path.join(OUT_DIR, os.path.splitext(src)[0] + suffix + ".o")

@@ -141,21 +141,25 @@ HG_DEV void acc_sqr(Acc& a, const Fp& x) {
     for (int j = i + 1; j < 10; j++) a.c[i + j] += (uint64_t)x.l[i] * d[j];
   }
 }
-// Montgomery REDC: r = T * 2^-286 mod p, canonical. Requires T < p R
-// (11 digits of 26 bits; the result T / R + q p / R < 2p before the final
-// conditional subtraction).
-HG_DEV void acc_reduce(Fp& r, Acc& a) {
+// One Montgomery REDC digit: q = c_i p' mod 2^26, c += q p 2^(26 i), and the
+// (now zero mod 2^26) column i carries into column i + 1.
+HG_DEV void acc_redc_digit(Acc& a, int i) {
+  const uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
 #pragma unroll
-  for (int i = 0; i < kRedcSteps; i++) {
-    uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
-#pragma unroll
-    for (int j = 0; j < 10; j++) {
-      a.c[i + j] += (uint64_t)q * p_limb(j);
-      asm("" : "+v"(a.c[i + j]));  // no reassociation into per-column chains
-    }
-    a.c[i + 1] += a.c[i] >> 26;
+  for (int j = 0; j < 10; j++) {
+    a.c[i + j] += (uint64_t)q * p_limb(j);
+    asm("" : "+v"(a.c[i + j]));  // no reassociation into per-column chains
   }
-  uint32_t x[10];
+  a.c[i + 1] += a.c[i] >> 26;
+}
+// digits FROM .. 10 (FROM > 0: acc_mad_redc ran the first ones)
+template <int FROM>
+HG_DEV void acc_redc_digits(Acc& a) {
+#pragma unroll
+  for (int i = FROM; i < kRedcSteps; i++) acc_redc_digit(a, i);
+}
+// columns 11..20 of a reduced accumulator as 10 limbs (the top one unmasked)
+HG_DEV void acc_redc_limbs(uint32_t (&x)[10], const Acc& a) {
   uint64_t carry = 0;
 #pragma unroll
   for (int j = 0; j < 10; j++) {
@@ -163,6 +167,33 @@ HG_DEV void acc_reduce(Fp& r, Acc& a) {
     x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
     carry = v >> 26;
   }
+}
+// a += x * y with the REDC digits interleaved, for the LAST product of a lazy
+// sum: once row i of x * y is in, column i is complete (earlier products are
+// whole, rows > i only reach higher columns), so digit i runs right there.
+// The reduction's serial chain (column i -> q_i -> 10 mads -> carry into
+// column i + 1) then overlaps the next rows' independent mads instead of
+// trailing all the products, where one wave per SIMD has nothing to hide it
+// behind. Digits 0..9; digit 10 follows (acc_reduce<10> and its wide forms).
+HG_DEV void acc_mad_redc(Acc& a, const Fp& x, const Fp& y) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      a.c[i + j] += (uint64_t)x.l[i] * y.l[j];
+      asm("" : "+v"(a.c[i + j]));
+    }
+    acc_redc_digit(a, i);
+  }
+}
+// Montgomery REDC: r = T * 2^-286 mod p, canonical. Requires T < p R
+// (11 digits of 26 bits; the result T / R + q p / R < 2p before the final
+// conditional subtraction). FROM: digits already done (acc_mad_redc).
+template <int FROM = 0>
+HG_DEV void acc_reduce(Fp& r, Acc& a) {
+  acc_redc_digits<FROM>(a);
+  uint32_t x[10];
+  acc_redc_limbs(x, a);
   fp_csub_rare(r, x);
 }
 

@@ -117,49 +117,21 @@ HG_DEV void fp_reduce8(Fp& r, const uint32_t* x) {
 // those pass through REDC unchanged, so the result is < (products / R) +
 // (linear terms) + p, below 31p (generator-checked); a quotient estimate
 // (fp_reduce8) makes it canonical. Sums of products only use acc_reduce.
+template <int FROM = 0>
 HG_DEV void acc_reduce_wide(Fp& r, Acc& a) {
-#pragma unroll
-  for (int i = 0; i < kRedcSteps; i++) {
-    uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
-#pragma unroll
-    for (int j = 0; j < 10; j++) {
-      a.c[i + j] += (uint64_t)q * p_limb(j);
-      asm("" : "+v"(a.c[i + j]));  // no reassociation into per-column chains
-    }
-    a.c[i + 1] += a.c[i] >> 26;
-  }
+  acc_redc_digits<FROM>(a);
   uint32_t x[10];
-  uint64_t carry = 0;
-#pragma unroll
-  for (int j = 0; j < 10; j++) {
-    uint64_t v = a.c[kRedcSteps + j] + carry;
-    x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
-    carry = v >> 26;
-  }
+  acc_redc_limbs(x, a);
   fp_reduce8(r, x);
 }
 
 // acc_reduce_wide without the final conditional subtraction: the quotient
 // estimate leaves the result in [0, 2p) (the lazy rounds, bn256_xprog.h)
+template <int FROM = 0>
 HG_DEV void acc_reduce_wide_lazy(Fp& r, Acc& a) {
-#pragma unroll
-  for (int i = 0; i < kRedcSteps; i++) {
-    uint32_t q = ((uint32_t)a.c[i] * kPInv26) & kMask;
-#pragma unroll
-    for (int j = 0; j < 10; j++) {
-      a.c[i + j] += (uint64_t)q * p_limb(j);
-      asm("" : "+v"(a.c[i + j]));
-    }
-    a.c[i + 1] += a.c[i] >> 26;
-  }
+  acc_redc_digits<FROM>(a);
   uint32_t x[10];
-  uint64_t carry = 0;
-#pragma unroll
-  for (int j = 0; j < 10; j++) {
-    uint64_t v = a.c[kRedcSteps + j] + carry;
-    x[j] = (j < 9) ? ((uint32_t)v & kMask) : (uint32_t)v;
-    carry = v >> 26;
-  }
+  acc_redc_limbs(x, a);
   constexpr uint32_t p9 = p_top_limb();
   const uint32_t q = x[9] / (p9 + 1u);
   int32_t c = 0;

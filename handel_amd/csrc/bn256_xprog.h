@@ -44,7 +44,7 @@ struct XHint {
 };
 struct XStream;
 template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ,
-          int EF>
+          int EF, int FU>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt);
 
 
@@ -178,8 +178,18 @@ HG_DEV void acc_mad_pinned(Acc& a, const Fp& x, const Fp& y) {
       asm("" : "+v"(a.c[i + j]));
     }
 }
-// a, b: the first product's operands, already loaded by the caller
-template <int W, int NP>
+// REDC digits interleaved with the job's last product (acc_mad_redc) where the
+// generator sets a round's FU flag (the pairing kernels' single-job rounds:
+// one wave per SIMD has nothing else to hide the reduction's serial chain
+// behind; the GT fold runs several waves per SIMD and keeps the
+// products-then-REDC order). HG_REDC_FUSE=0 builds that order everywhere.
+#ifndef HG_REDC_FUSE
+#define HG_REDC_FUSE 1
+#endif
+
+// a, b: the first product's operands, already loaded by the caller.
+// FUSE: the last product runs with REDC digits 0..9 (acc_mad_redc).
+template <int W, int NP, bool FUSE>
 HG_DEV void x_products(const Team& T, const uint32_t (&w)[W], int base, Acc& acc, Fp a, Fp b) {
   if constexpr (NP > 0) {
     x_for<NP>([&](auto p) {
@@ -188,7 +198,8 @@ HG_DEV void x_products(const Team& T, const uint32_t (&w)[W], int base, Acc& acc
         ld_fp_a8(a2, x_at(T, x_off(w, base + 2 * (p + 1))));
         ld_fp_a8(b2, x_at(T, x_off(w, base + 2 * (p + 1) + 1)));
       }
-      acc_mad_pinned(acc, a, b);
+      if constexpr (FUSE && p + 1 == NP) acc_mad_redc(acc, a, b);
+      else acc_mad_pinned(acc, a, b);
       // pin the columns here: the mads of product p stay in this region
       // (and are not sunk past the store's branch with the rest of the job)
 #pragma unroll
@@ -232,12 +243,15 @@ HG_DEV void kacc_mad_pinned(KAcc& k, const Fp& x, const Fp& y) {
       asm("" : "+v"(k.z1[i + j]));
     }
 }
-template <int W, int NP>
+// FUSE: products 0 .. NP - 2 as above, the last one schoolbook with REDC
+// digits 0..9 interleaved (acc_mad_redc), after the half products combined
+template <int W, int NP, bool FUSE>
 HG_DEV void x_products_ks(const Team& T, const uint32_t (&w)[W], int base, Acc& acc, Fp a, Fp b) {
+  constexpr int NK = FUSE ? NP - 1 : NP;  // Karatsuba products
   KAcc k;
 #pragma unroll
   for (int c = 0; c < 9; c++) k.z0[c] = k.z1[c] = k.z2[c] = 0;
-  x_for<NP>([&](auto p) {
+  x_for<NK>([&](auto p) {
     Fp a2, b2;
     if constexpr (p + 1 < NP) {
       ld_fp_a8(a2, x_at(T, x_off(w, base + 2 * (p + 1))));
@@ -258,11 +272,12 @@ HG_DEV void x_products_ks(const Team& T, const uint32_t (&w)[W], int base, Acc& 
     acc.c[c + 10] += k.z2[c];
     acc.c[c + 5] += k.z1[c] - (k.z0[c] + k.z2[c]);
   }
+  if constexpr (FUSE) acc_mad_redc(acc, a, b);  // a, b: the last product's operands
 }
 
 // EF: a0, b0 already hold the first product's operands (read before the
 // pre-pass: plain elements, see x_round)
-template <int W, int NP, int NL, int KL, int KS, int LZ = 0, int EF = 0>
+template <int W, int NP, int NL, int KL, int KS, int LZ = 0, int EF = 0, int FU = 0>
 HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32_t& dst, Fp a0 = Fp{},
                   Fp b0 = Fp{}) {
   Acc acc;
@@ -282,12 +297,14 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 #pragma unroll
     for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] = val[l];
   }
-  if constexpr (KS) x_products_ks<W, NP>(T, w, base, acc, a0, b0);
-  else x_products<W, NP>(T, w, base, acc, a0, b0);
+  constexpr bool FUSE = HG_REDC_FUSE && FU && NP > 0;
+  constexpr int FROM = FUSE ? 10 : 0;  // REDC digits the products already ran
+  if constexpr (KS) x_products_ks<W, NP, FUSE>(T, w, base, acc, a0, b0);
+  else x_products<W, NP, FUSE>(T, w, base, acc, a0, b0);
   dst = x_off(w, base + lbase + NL);
-  if constexpr (NL > 0 && LZ) acc_reduce_wide_lazy(r, acc);  // linear terms, lazy: [0, 2p)
-  else if constexpr (NL > 0) acc_reduce_wide(r, acc);       // linear terms: result < 31p
-  else acc_reduce(r, acc);                                  // products only: < 2p, one subtraction
+  if constexpr (NL > 0 && LZ) acc_reduce_wide_lazy<FROM>(r, acc);  // linear terms, lazy: [0, 2p)
+  else if constexpr (NL > 0) acc_reduce_wide<FROM>(r, acc);       // linear terms: result < 31p
+  else acc_reduce<FROM>(r, acc);                                  // products only: < 2p, one subtraction
 }
 
 // One round. Table layout per lane (16-bit entries): NV x (dst, NT x term),
@@ -296,7 +313,7 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
 // read before either result is stored, so in-place programs are fine.
 // off: the round's table offset
 template <int NV, int NT, int NP, int NL, int W, int NP2, int NL2, int KP, int KL1, int KL2, int KS1, int KS2, int LZ,
-          int EF>
+          int EF, int FU>
 HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   if (S.off != off) x_fetch(T, S, XHint{off, W});  // wave-uniform; only without a (correct) hint
   uint32_t w[W];
@@ -336,8 +353,8 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
   }
   Fp r;
   uint32_t dst;
-  if constexpr (EF) x_job<W, NP, NL, KL1, KS1, LZ, EF>(T, w, jbase, r, dst, e0, e1);
-  else x_job<W, NP, NL, KL1, KS1, LZ>(T, w, jbase, r, dst);
+  if constexpr (EF) x_job<W, NP, NL, KL1, KS1, LZ, EF, FU>(T, w, jbase, r, dst, e0, e1);
+  else x_job<W, NP, NL, KL1, KS1, LZ, 0, FU>(T, w, jbase, r, dst);
   if constexpr (NP2 > 0 || NL2 > 0) {
     Fp r2;
     uint32_t dst2;

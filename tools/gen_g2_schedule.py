@@ -1306,8 +1306,11 @@ def emit_x(X, path):
             nxt = f"XHint{{{rounds[i + 1][1]}, {rounds[i + 1][0].words()}}}" if i + 1 < len(rounds) else "h"
             lz = int(name in LAZY_PROGRAMS and bx.nl > 0)
             assert not (lz and bx.fused), "a lazy round is not fused"
+            # FU: REDC interleaved with the last product (bn256_xprog.h x_job):
+            # the pairing kernels' single-job rounds, not the GT fold's
+            fu = int(ctx != "FOLD" and not bx.fused)
             calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
-                         f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}, {bx.ef}>(T, S, {off}, {nxt});")
+                         f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}, {bx.ef}, {fu}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
         targs = f"XP_{name}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
