@@ -1307,8 +1307,11 @@ def emit_x(X, path):
             lz = int(name in LAZY_PROGRAMS and bx.nl > 0)
             assert not (lz and bx.fused), "a lazy round is not fused"
             # FU: REDC interleaved with the last product (bn256_xprog.h x_job):
-            # the pairing kernels' single-job rounds, not the GT fold's
-            fu = int(ctx != "FOLD" and not bx.fused)
+            # the final exponentiation's and the sig-only Miller loop's rounds;
+            # not the GT fold's (several waves per SIMD hide the chain), not
+            # two-job rounds, not the pk-side G2 steps (measured: config 2
+            # 0.5 % slower with them, profiles/r03fuse_redc_ab.json)
+            fu = int(not bx.fused and (ctx == "FE" or name in SIG_PROGRAMS))
             calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
                          f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}, {bx.ef}, {fu}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
