@@ -139,7 +139,7 @@ __global__ __launch_bounds__(64) void k_gt_keys(const PointG2* reg, int n, const
   }
   XStream S = x_stream();
   team_miller_check(T, F, C, tab, false, S, final_exp_hint());
-  team_final_exp(T, F, S);
+  team_final_exp_fc(T, F, S);  // the GT tables: FE^m (team_final_exp_fc)
   if (valid) gt_store(T, S_F, out + idx);
 }
 
@@ -667,7 +667,7 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
   else sg = sigs[ci];
   XStream S = x_stream();
   team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, final_exp_hint());
-  team_final_exp(T, F, S);
+  team_final_exp_fc(T, F, S);
   if (kStore) {
     team_sync();
     if (valid) gt_store(T, S_F, fe + idx);

@@ -87,6 +87,79 @@ HG_DEV void team_final_exp(const Team& T, uint32_t* F, XStream& S) {
   x_mul12<S_F, S_K, S_J>(T, S, xh_none());                      // result
   DIAG_ADD(6);
 }
+// The easy part (f^((p^6 - 1)(p^2 + 1))) of both final exponentiations: the
+// result in slot F. h: the program after it.
+HG_DEV void team_final_exp_easy(const Team& T, XStream& S, XHint h) {
+  t12_inv_x<S_A, S_F, S_K, S_L>(T, S, xh<IMul12<S_F, S_B, S_A>>());  // A = f^-1
+  t12_conj(T, S_B, S_F);                                        // B = conj(f)
+  x_mul12<S_F, S_B, S_A>(T, S, xh<IMul12<S_F, S_F, S_A>>());   // t1 = f^(p^6 - 1)
+  t12_frob2(T, S_A, S_F);
+  x_mul12<S_F, S_F, S_A>(T, S, h);                              // t1 = t1^(p^2 + 1)
+}
+
+// FE(f)^m with m = 2u(6u^2 + 3u + 1), coprime to r: the hard part of
+// Fuentes-Castaneda, Knapp and Rodriguez-Henriquez ("Faster hashing to G2",
+// SAC 2011, the BN chain of Duquesne-Ghammam eprint 2015/192 as gnark's bn254
+// runs it): three exponentiations by u, 10 multiplications and 3 cyclotomic
+// squarings instead of x/crypto's 13 and 4. x -> x^m is a bijection of the
+// order-r group GT, so equalities and "== 1" tests of FE values are the same
+// with either chain, as long as both sides use this one: k_gt_keys (the GT
+// tables), k_verify_sig and k_verify. k_pair and the Fp12 probe keep
+// x/crypto's chain (team_final_exp), whose values are compared byte for byte
+// with the reference's GT marshal. Oracle: bn256_oracle.final_exponentiation_fc.
+//
+// The three exponentiations share one copy of the exp-by-v loop (I <-> J,
+// base in I, result in J); phase ph prepares the next base between them.
+// Slots: F = res, A = t0, B = t1, C = t2, D = t3, E = t4, G scratch, K = the
+// exp-by-v scratch. Every input of a hand-written helper (conj, frob, copy)
+// is a MUL12 result (canonical); the one squaring that feeds an
+// exponentiation's conj is the canonical CYC_SQR program.
+HG_DEV void team_final_exp_fc(const Team& T, uint32_t* F, XStream& S) {
+  DIAG_T0();
+  team_final_exp_easy(T, S, xh<ICyc<S_J, S_I>>());
+  DIAG_ADD(5);
+  t12_copy(T, S_I, S_F);  // base of the first exponentiation: res
+#pragma unroll 1
+  for (int ph = 0; ph < 3; ph++) {
+#pragma unroll 1
+    for (int st = 0; st < 3; st++) {  // J = I^v, I = J^v, J = I^v
+      const XHint next = st < 2 ? ((st & 1) ? xh<ICyc<S_J, S_I>>() : xh<ICyc<S_I, S_J>>())
+                                : (ph == 0 ? xh<ICyc<S_A, S_A>>() : ph == 1 ? xh<IMul12<S_B, S_C, S_D>>()
+                                                                            : xh<IMul12<S_E, S_B, S_J>>());
+      if ((st & 1) == 0) t12_pow_v_x<S_J, S_I>(T, S, next);
+      else t12_pow_v_x<S_I, S_J>(T, S, next);
+    }
+    if (ph == 0) {  // t0 = conj(res^u)^2, t1 = t0^2 t0; next base t1
+      t12_conj(T, S_A, S_J);
+      x_cyc_sqr<S_A, S_A>(T, S, xh<ICyc<S_B, S_A>>());
+      x_cyc_sqr<S_B, S_A>(T, S, xh<IMul12<S_B, S_A, S_B>>());
+      x_mul12<S_B, S_A, S_B>(T, S, xh<ICyc<S_J, S_I>>());
+      t12_copy(T, S_I, S_B);
+    } else if (ph == 1) {  // t2 = conj(t1^u), t1 = t2 conj(t1); next base t3 = t2^2
+      t12_conj(T, S_C, S_J);
+      t12_conj(T, S_D, S_B);
+      x_mul12<S_B, S_C, S_D>(T, S, xh<ICyc0<S_I, S_C>>());
+      ICyc0<S_I, S_C>::run(T, S, xh<ICyc<S_J, S_I>>());
+    } else {  // t4 = t1 t3^u
+      x_mul12<S_E, S_B, S_J>(T, S, xh<IMul12<S_D, S_A, S_E>>());
+    }
+  }
+  DIAG_ADD(7);
+  x_mul12<S_D, S_A, S_E>(T, S, xh<IMul12<S_A, S_C, S_E>>());  // t3 = t0 t4
+  x_mul12<S_A, S_C, S_E>(T, S, xh<IMul12<S_A, S_F, S_A>>());  // t0 = t2 t4
+  x_mul12<S_A, S_F, S_A>(T, S, xh<IMul12<S_A, S_G, S_A>>());  // t0 = res t0
+  t12_frob(T, S_G, S_D);
+  x_mul12<S_A, S_G, S_A>(T, S, xh<IMul12<S_A, S_G, S_A>>());  // t0 = frob(t3) t0
+  t12_frob2(T, S_G, S_E);
+  x_mul12<S_A, S_G, S_A>(T, S, xh<IMul12<S_G, S_G, S_D>>());  // t0 = frob2(t4) t0
+  t12_conj(T, S_G, S_F);
+  x_mul12<S_G, S_G, S_D>(T, S, xh<IMul12<S_F, S_G, S_A>>());  // t2 = conj(res) t3
+  t12_frob(T, S_G, S_G);
+  t12_frob2(T, S_G, S_G);                                       // t2 = frob^3(t2)
+  x_mul12<S_F, S_G, S_A>(T, S, xh_none());                      // result
+  DIAG_ADD(6);
+}
+
 // the first program team_final_exp runs (t12_inv_x<S_A, S_F, S_K, S_L>)
 HG_DEV constexpr XHint final_exp_hint() { return xh<IMul12<S_L, S_F, S_K>>(); }
 

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const L
 #ifdef HG_DIAG
   uint64_t diag_mid = __builtin_amdgcn_s_memtime();
 #endif
-  team_final_exp(T, F, S);
+  team_final_exp_fc(T, F, S);  // FE^m == 1 <=> FE == 1
   bool ok = t12_is_one(T, S_F);
   if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
 #ifdef HG_DIAG

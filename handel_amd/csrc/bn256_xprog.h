@@ -376,6 +376,8 @@ using IMul12 = XInst<XP_MUL12, D, A, B>;
 template <int D, int A>
 using ICyc = XInst<XP_CYC_SQR_X, D, A>;
 template <int D, int A>
+using ICyc0 = XInst<XP_CYC_SQR, D, A>;  // canonical result (CYC_SQR_X's is lazy)
+template <int D, int A>
 using ISqr12 = XInst<XP_SQR12, D, A>;
 template <int D, int A>
 using ILinePk = XInst<XP_LINE_PK, D, A>;

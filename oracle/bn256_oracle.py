@@ -668,6 +668,30 @@ def final_exponentiation(f):
     return f12_mul(t0, t1)
 
 
+def final_exponentiation_fc(f):
+    """FE(f)^m, m = 2u(6u^2 + 3u + 1) (coprime to the group order): the BN hard
+    part of Fuentes-Castaneda, Knapp and Rodriguez-Henriquez (SAC 2011) in the
+    form gnark's bn254 runs it (Duquesne-Ghammam, eprint 2015/192). Not the
+    reference's chain: the GPU's GT tables, its sig-side pairing and its
+    two-pairing check use it (team_final_exp_fc), where only equalities between
+    values of the same chain, or with 1, are tested."""
+    t1 = f12_mul(f12_conj(f), f12_inv(f))
+    res = f12_mul(t1, f12_frob2(t1))
+    t0 = f12_sqr(f12_conj(f12_pow(res, U)))
+    t1 = f12_mul(t0, f12_sqr(t0))
+    t2 = f12_conj(f12_pow(t1, U))
+    t1 = f12_mul(t2, f12_conj(t1))
+    t4 = f12_mul(t1, f12_pow(f12_sqr(t2), U))
+    t3 = f12_mul(t0, t4)
+    t0 = f12_mul(res, f12_mul(t2, t4))
+    t0 = f12_mul(f12_frob2(t4), f12_mul(f12_frob(t3), t0))
+    t2 = f12_frob(f12_frob2(f12_mul(f12_conj(res), t3)))
+    return f12_mul(t2, t0)
+
+
+FC_EXPONENT = 2 * U * (6 * U * U + 3 * U + 1)  # final_exponentiation_fc = FE^FC_EXPONENT
+
+
 def pair(g1, g2):
     """bn256.Pair(g1, g2): optimalAte, with GT = 1 if either input is infinity."""
     if g1 is None or g2 is None:

@@ -112,6 +112,22 @@ def test_normalised_g2base_lines_give_the_same_pairing():
     assert O.final_exponentiation(_miller_normalised(O.G1_GEN, unit=True)) == O.F12_ONE
 
 
+def test_final_exponentiation_fc_is_a_fixed_power():
+    """The GPU's hard part (Fuentes-Castaneda et al.): FE^m with m coprime to
+    the group order, so x -> x^m is a bijection of GT and equality tests agree
+    with the reference's chain, for pairing values and arbitrary elements."""
+    import math
+    import random
+    m = O.FC_EXPONENT
+    assert math.gcd(m, O.ORDER) == 1
+    rng = random.Random(11)
+    f1 = O.miller(O.g2_mul(O.G2_GEN, 5), O.g1_mul(O.G1_GEN, 7))
+    f2 = [(rng.randrange(O.P), rng.randrange(O.P)) for _ in range(6)]
+    for f in (f1, f2):
+        assert O.final_exponentiation_fc(f) == O.f12_pow(O.final_exponentiation(f), m)
+    assert O.final_exponentiation_fc(O.F12_ONE) == O.F12_ONE
+
+
 def test_bilinearity_and_nondegeneracy():
     e = O.pair(O.G1_GEN, O.G2_GEN)
     assert not O.f12_is_one(e)

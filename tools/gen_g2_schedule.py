@@ -1151,6 +1151,10 @@ INSTANCES = sorted(set(
     + [(f"PADD_{v}_{i}", ()) for v in ("POS", "NEG", "F1", "F2") for i in (1, 3)]
     + [(f"MADD_{v}_2", ("F", "F")) for v in ("POS", "NEG", "F1", "F2")]
     + [("MDBL_1", ("F", "F")), ("MDBL_2", ("F", "F"))]
+    # team_final_exp_fc (bn256_pairing.h): the Fuentes-Castaneda hard part
+    + [("CYC_SQR_X", ("B", "A")), ("CYC_SQR", ("I", "C"))]
+    + [("MUL12", b) for b in [("B", "A", "B"), ("B", "C", "D"), ("E", "B", "J"), ("D", "A", "E"), ("A", "C", "E"),
+                              ("A", "F", "A"), ("A", "G", "A"), ("G", "G", "D"), ("F", "G", "A")]]
     # bn256_gt.hip: the sig-only Miller loop and the GT fold
     + [("SDBL", ("F", "F")), ("LFEV", ("F", "F")), ("FEVAL", ()), ("MUL12F", ("A", "A", "B"))]))
 
@@ -1250,7 +1254,7 @@ def check_instances(X, seed=3):
 # the programs k_verify_sig runs (bn256_gt.hip: the sig-only Miller loop and
 # the final exponentiation); its team region ends after the last element they
 # (and the hand-written helpers: registers up to FC) touch
-SIG_PROGRAMS = ("SDBL", "LFEV", "FEVAL", "LINE_FIX", "MUL12", "CYC_SQR_X")
+SIG_PROGRAMS = ("SDBL", "LFEV", "FEVAL", "LINE_FIX", "MUL12", "CYC_SQR_X", "CYC_SQR")
 
 
 def touched(bx):
