@@ -551,6 +551,16 @@ static void miller(fp12* f, const fp2* qx2, const fp2* qy2, const fp* px, const 
  * G1-dependent factors left out (b = bx * Px, c = cy * Py). */
 #define NLINES 85
 static fp2 G2L_A[NLINES], G2L_BX[NLINES], G2L_CY[NLINES];
+/* the same lines divided by a (the GPU's table, bn256_kernels.hip k_g2_lines) */
+static fp2 G2N_BX[NLINES], G2N_CY[NLINES];
+static void build_g2_lines_n(void) {
+  for (int s = 0; s < NLINES; s++) {
+    fp2 ai;
+    f2_inv(&ai, &G2L_A[s]);
+    f2_mul(&G2N_BX[s], &G2L_BX[s], &ai);
+    f2_mul(&G2N_CY[s], &G2L_CY[s], &ai);
+  }
+}
 static void build_g2_lines(void) {
   g2p r;
   fp2 r2, mqy;
@@ -585,10 +595,53 @@ static inline void fixed_line(fp12* f, int s, const fp* sx, const fp* nsy) {
   f2_muls(&c, &G2L_CY[s], nsy);
   f12_mul_line(f, &G2L_A[s], &b, &c);
 }
+/* f *= c + b w + w^3 (a normalised line): L1 = (b, 1, 0), so the sparse
+ * Karatsuba product loses the multiplications by a: 9 Fp2 multiplications. */
+static void f6_mul_by_01_n(fp6* r, const fp6* a, const fp2* b0) {
+  fp2 v0, t, s;
+  f2_mul(&v0, &a->c[0], b0);
+  fp6 o;
+  f2_add(&t, &a->c[1], &a->c[2]);
+  f2_sub(&t, &t, &a->c[1]);
+  f2_mul_xi(&t, &t);
+  f2_add(&o.c[0], &t, &v0);
+  f2_add(&t, &a->c[0], &a->c[1]);
+  s = *b0;
+  f2_add(&s, &s, &F2_ONE);
+  f2_mul(&t, &t, &s);
+  f2_sub(&t, &t, &v0);
+  f2_sub(&o.c[1], &t, &a->c[1]);
+  f2_add(&t, &a->c[0], &a->c[2]);
+  f2_mul(&t, &t, b0);
+  f2_sub(&t, &t, &v0);
+  f2_add(&o.c[2], &t, &a->c[1]);
+  *r = o;
+}
+static void f12_mul_line_n(fp12* f, const fp2* b, const fp2* c) {
+  fp6 A, B, t0, t1, S;
+  split12(f, &A, &B);
+  for (int i = 0; i < 3; i++) f2_mul(&t0.c[i], &A.c[i], c);
+  f6_mul_by_01_n(&t1, &B, b);
+  f6_add(&S, &A, &B);
+  fp2 cb;
+  f2_add(&cb, c, b);
+  f6_mul_by_01_n(&S, &S, &cb);
+  f6_sub(&S, &S, &t0);
+  f6_sub(&S, &S, &t1);
+  f6_mul_tau(&t1, &t1);
+  f6_add(&t0, &t0, &t1);
+  join12(f, &t0, &S);
+}
+static inline void fixed_line_n(fp12* f, int s, const fp* sx, const fp* nsy) {
+  fp2 b, c;
+  f2_muls(&b, &G2N_BX[s], sx);
+  f2_muls(&c, &G2N_CY[s], nsy);
+  f12_mul_line_n(f, &b, &c);
+}
 /* Multi-Miller loop of the verification product e(P, Q) * e(-S, G2Base):
  * shared squarings, on-the-fly lines for Q, table lines for G2Base. */
 static void miller2(fp12* f, int use_q, const fp2* qx2, const fp2* qy2, const fp* px, const fp* py, int use_s,
-                    const fp* sx, const fp* sy) {
+                    const fp* sx, const fp* sy, int norm) {
   g2p r;
   fp2 a, b, c, r2, mqy;
   fp nsy;
@@ -604,7 +657,7 @@ static void miller2(fp12* f, int use_q, const fp2* qx2, const fp2* qy2, const fp
       line_double(&a, &b, &c, &r, px, py);
       f12_mul_line(f, &a, &b, &c);
     }
-    if (use_s) fixed_line(f, s, sx, &nsy);
+    if (use_s) (norm ? fixed_line_n : fixed_line)(f, s, sx, &nsy);
     s++;
     int d = NAF[i - 1];
     if (d == 0) continue;
@@ -612,7 +665,7 @@ static void miller2(fp12* f, int use_q, const fp2* qx2, const fp2* qy2, const fp
       line_add(&a, &b, &c, &r, qx2, d > 0 ? qy2 : &mqy, px, py, &r2);
       f12_mul_line(f, &a, &b, &c);
     }
-    if (use_s) fixed_line(f, s, sx, &nsy);
+    if (use_s) (norm ? fixed_line_n : fixed_line)(f, s, sx, &nsy);
     s++;
   }
   if (use_q) {
@@ -630,8 +683,8 @@ static void miller2(fp12* f, int use_q, const fp2* qx2, const fp2* qy2, const fp
     f12_mul_line(f, &a, &b, &c);
   }
   if (use_s) {
-    fixed_line(f, s, sx, &nsy);
-    fixed_line(f, s + 1, sx, &nsy);
+    (norm ? fixed_line_n : fixed_line)(f, s, sx, &nsy);
+    (norm ? fixed_line_n : fixed_line)(f, s + 1, sx, &nsy);
   }
 }
 
@@ -674,6 +727,42 @@ static void final_exp(fp12* out, const fp12* in) {
   f12_mul(&t1, &t1, &y0);
   f12_sqr(&t0, &t0);
   f12_mul(out, &t0, &t1);
+}
+
+/* FE(f)^m, m = 2u(6u^2 + 3u + 1): the GPU's hard part (Fuentes-Castaneda,
+ * Knapp, Rodriguez-Henriquez 2011; bn256_oracle.final_exponentiation_fc),
+ * 10 Fp12 multiplications after the three exponentiations instead of 13 */
+static void final_exp_fc(fp12* out, const fp12* in) {
+  fp12 res, inv, t0, t1, t2, t3, t4;
+  f12_conj(&t1, in);
+  f12_inv(&inv, in);
+  f12_mul(&t1, &t1, &inv);
+  f12_frob2(&t2, &t1);
+  f12_mul(&res, &t1, &t2);
+  f12_pow_u(&t0, &res);
+  f12_conj(&t0, &t0);
+  f12_sqr(&t0, &t0);
+  f12_sqr(&t1, &t0);
+  f12_mul(&t1, &t0, &t1);
+  f12_pow_u(&t2, &t1);
+  f12_conj(&t2, &t2);
+  f12_conj(&t3, &t1);
+  f12_mul(&t1, &t2, &t3);
+  f12_sqr(&t3, &t2);
+  f12_pow_u(&t4, &t3);
+  f12_mul(&t4, &t1, &t4);
+  f12_mul(&t3, &t0, &t4);
+  f12_mul(&t0, &t2, &t4);
+  f12_mul(&t0, &res, &t0);
+  f12_frob(&t2, &t3);
+  f12_mul(&t0, &t2, &t0);
+  f12_frob2(&t2, &t4);
+  f12_mul(&t0, &t2, &t0);
+  f12_conj(&t2, &res);
+  f12_mul(&t2, &t2, &t3);
+  f12_frob2(&t2, &t2);
+  f12_frob(&t2, &t2);
+  f12_mul(out, &t2, &t0);
 }
 
 /* ------------------------------------------------------------------ group law */
@@ -1011,6 +1100,7 @@ void ref_init(void) {
   XI_P12 = GAMMA1[3];  /* xi^((p-1)/2) */
   XI_PSQ13 = GAMMA2[2]; /* xi^((p^2-1)/3) */
   build_g2_lines();
+  build_g2_lines_n();
   g_inited = 1;
 }
 
@@ -1164,10 +1254,14 @@ static int verify_points(const g1p* hm, int pk_inf, const fp2* qx, const fp2* qy
                          const fp* sx, const fp* sy, int fast) {
   fp hx = hm->x, hy = hm->y; /* affine (hash_point normalises) */
   fp12 f1, f2_, e1, e2;
-  if (fast == 2) {
-    /* the algorithm the GPU runs: one multi-Miller loop + one final exp */
-    miller2(&f1, !pk_inf, qx, qy, &hx, &hy, !sig_inf, sx, sy);
-    final_exp(&e1, &f1);
+  if (fast >= 2) {
+    /* one multi-Miller loop + one final exp: fast = 2 with x/crypto's lines and
+     * chain (the r01/r02 GPU algorithm), fast = 3 the GPU's algorithm since r03
+     * (normalised G2Base lines, the Fuentes-Castaneda hard part): FE^m == 1
+     * <=> FE == 1, and the lines' Fp2 factors are killed by the exponentiation */
+    miller2(&f1, !pk_inf, qx, qy, &hx, &hy, !sig_inf, sx, sy, fast == 3);
+    if (fast == 3) final_exp_fc(&e1, &f1);
+    else final_exp(&e1, &f1);
     return f12_is_one(&e1) ? RC_OK : RC_SIG_INVALID;
   }
   if (!fast) {

@@ -239,26 +239,29 @@ def test_rehash_per_check_matches_batch_hash():
 
 
 def test_algorithmic_work_per_check_is_pinned():
-    """bench.py's roofline work figure = the oracle's op counter for one check
-    of the algorithm the GPU runs (fast=2)."""
+    """bench.py's work figures = the oracle's op counter for one check: the
+    reference's product-form check (fast=2, effective_rate) and the algorithm
+    k_verify runs (fast=3: normalised G2Base lines, Fuentes-Castaneda hard
+    part)."""
     import bench
 
     L = R.lib()
     L.ref_fp_mul_count.restype = ctypes.c_uint64
     _, pks, sigs = F.keys_and_sigs(3, seed=b"cnt")
-    counts = []
-    for n in (1, 3):
-        L.ref_reset_count(1)
-        R.verify_batch(F.LIB_MESSAGE, pks[:128 * n], sigs[:64 * n], nthreads=1, fast=2)
-        counts.append(L.ref_fp_mul_count())
-    L.ref_reset_count(0)
-    assert (counts[1] - counts[0]) // 2 == bench.FPMUL_PER_CHECK
+    for fast, want in ((2, bench.FPMUL_REFERENCE_CHECK), (3, bench.FPMUL_PER_CHECK)):
+        counts = []
+        for n in (1, 3):
+            L.ref_reset_count(1)
+            R.verify_batch(F.LIB_MESSAGE, pks[:128 * n], sigs[:64 * n], nthreads=1, fast=fast)
+            counts.append(L.ref_fp_mul_count())
+        L.ref_reset_count(0)
+        assert (counts[1] - counts[0]) // 2 == want
 
 
 def test_sig_pairing_work_is_pinned():
     """The GT path's check kernel (k_verify_sig) runs one pairing, G2Base at
     -sig, and its final exponentiation: the oracle's count of the same check
-    with the pk side off (pk = infinity) is bench.FPMUL_PER_SIG_PAIRING."""
+    with the pk side off (pk = infinity, fast=3) is bench.FPMUL_PER_SIG_PAIRING."""
     import bench
 
     L = R.lib()
@@ -268,7 +271,7 @@ def test_sig_pairing_work_is_pinned():
     counts = []
     for n in (1, 3):
         L.ref_reset_count(1)
-        R.verify_batch(F.LIB_MESSAGE, inf[:128 * n], sigs[:64 * n], nthreads=1, fast=2)
+        R.verify_batch(F.LIB_MESSAGE, inf[:128 * n], sigs[:64 * n], nthreads=1, fast=3)
         counts.append(L.ref_fp_mul_count())
     L.ref_reset_count(0)
     assert (counts[1] - counts[0]) // 2 == bench.FPMUL_PER_SIG_PAIRING
