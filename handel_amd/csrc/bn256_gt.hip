@@ -215,10 +215,10 @@ __global__ __launch_bounds__(64) void k_gt_cross(int nwin, Gt* win) {
 // 16-key windows: entry (hi << 8) | lo = w8[2w][lo] * w8[2w + 1][hi]; one
 // team per (window, hi), 256 products, the next left operand in flight.
 __global__ __launch_bounds__(64) void k_gt_win16(const Gt* w8, int nwin8, int nwin16, Gt* w16) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
-  Team T = make_team(lds, kFoldWords);
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams12 * kFoldWords];
+  Team T = make_team12(lds, kFoldWords);  // five 12-lane teams per wave
   fold_regs_init(T);
-  const int task = blockIdx.x * 4 + ((threadIdx.x & 63) >> 4);
+  const int task = blockIdx.x * kTeams12 + team12_index();
   const bool valid = task < 256 * nwin16;
   const int w = valid ? task >> 8 : 0, hi = task & 255;
   const Gt* lo_tab = w8 + (size_t)(2 * w) * 256;
@@ -442,15 +442,15 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
 __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, const uint32_t* terms,
                                                   const int2* ord, int cap, const GtReq* plan, const GtHdr* hdr,
                                                   int chunk, Gt* partial, Gt* y) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kFoldWords];
-  Team T = make_team(lds, kFoldWords);
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams12 * kFoldWords];
+  Team T = make_team12(lds, kFoldWords);  // five 12-lane teams per wave
   fold_regs_init(T);
-  const int team = (threadIdx.x & 63) >> 4;
+  const int team = team12_index();
   const int total = hdr->chunks, nlong = hdr->nlong;
   XStream S = x_stream();
-  for (int base = blockIdx.x * 4; base < total; base += gridDim.x * 4) {  // wave-uniform
+  for (int base = blockIdx.x * kTeams12; base < total; base += gridDim.x * kTeams12) {  // wave-uniform
     const int k = base + team;
-    const bool valid = k < total;
+    const bool valid = k < total && T.active;
     int first = 0, cnt = 0, r = 0, c = 0;
     bool single = false;
     if (valid) {
@@ -464,15 +464,15 @@ __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, 
     }
     int maxc = cnt;
 #pragma unroll
-    for (int d = 16; d < 64; d <<= 1) maxc = max(maxc, __shfl_xor(maxc, d));
+    for (int d = 1; d < 64; d <<= 1) maxc = max(maxc, __shfl_xor(maxc, d));
     // the chunk's term words, read once: lane tl of the team holds term tl
-    // (terms past 16 are read from the list), so no table read waits on a
+    // (terms past 12 are read from the list), so no table read waits on a
     // dependent index load
     const uint32_t my_t = T.tl < cnt ? terms[first + T.tl] : 0u;
-    const int tbase = threadIdx.x & 48;
+    const int tbase = 12 * team;
     auto term = [&](int i) -> uint32_t {  // wave-uniform i: every lane runs the shuffle
-      const uint32_t v = (uint32_t)__shfl((int)my_t, tbase + (i & 15), 64);
-      return i < 16 ? v : (i < cnt ? terms[first + i] : 0u);
+      const uint32_t v = (uint32_t)__shfl((int)my_t, tbase + (i < 12 ? i : 0), 64);
+      return i < 12 ? v : (i < cnt ? terms[first + i] : 0u);
     };
     Fp cur, n1, n2, one;
     gt_one_value(one, T);
@@ -735,7 +735,7 @@ void launch_gt_windows8(const Gt* key, int nreg, Gt* w8, int nwin8, hipStream_t 
   k_gt_cross<<<nblk(15 * nwin8, 4), 64, 0, s>>>(nwin8, w8);
 }
 void launch_gt_windows16(const Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s) {
-  if (nwin16 > 0) k_gt_win16<<<nblk(256 * nwin16, 4), 64, 0, s>>>(w8, nwin8, nwin16, w16);
+  if (nwin16 > 0) k_gt_win16<<<nblk(256 * nwin16, kTeams12), 64, 0, s>>>(w8, nwin8, nwin16, w16);
 }
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s) {
   if (ndst > 0) k_gt_blocks<<<nblk(ndst, 4), 64, 0, s>>>(src, stride, nsrc, dst, ndst);

@@ -96,6 +96,27 @@ HG_DEV Team make_team(uint32_t* lds_base, int words_per_team) {
   return T;
 }
 
+// Five 12-lane teams per wave (lanes 12 t .. 12 t + 11; lanes 60..63 are
+// team 4's idle lanes 12..15): for programs whose pre-pass values live on
+// lanes 0..11 (the generator's PRE_LANES: MUL12F), the GT fold's chunk kernel
+// then runs 5 products per wave instruction stream instead of 4.
+static constexpr int kTeams12 = 5;
+HG_DEV int team12_index() {
+  const int l = threadIdx.x & 63;
+  return l < 60 ? l / 12 : 4;
+}
+HG_DEV Team make_team12(uint32_t* lds_base, int words_per_team) {
+  Team T;
+  const int team = team12_index();
+  T.tl = (threadIdx.x & 63) - 12 * team;
+  T.base = lds_base + team * words_per_team;
+  T.active = T.tl < 12;
+  T.e = T.active ? T.tl : 11;
+  T.k = T.e >> 1;
+  T.comp = T.e & 1;
+  return T;
+}
+
 // Reduce a normalized-limb value < 31p (limb 9 holds the top bits) to [0, p):
 // q = floor(top / (p9 + 1)) underestimates floor(value / p) by at most one,
 // so one conditional subtraction finishes.

@@ -729,7 +729,9 @@ class XRound:
         return b
 
 
-def compile_round(lanes, name, scratch_cap, lanes2=None):
+def compile_round(lanes, name, scratch_cap, lanes2=None, pre_lanes=16):
+    """pre_lanes: lanes that evaluate the pre-pass values (16, or 12 for
+    programs that also run in 12-lane teams: PRE_LANES)."""
     one_lc = [(REG["ONE"], 1)]
     values = {}      # canonical lincomb -> scratch code
     order = []
@@ -779,7 +781,7 @@ def compile_round(lanes, name, scratch_cap, lanes2=None):
             assert not ({u for u, v in p2} | {v for u, v in p2} | {s for s, _ in l2}) & d1, name
     nvals = len(order)
     assert nvals <= scratch_cap, f"{name}: {nvals} pre-pass values > scratch {scratch_cap}"
-    nv = (nvals + 15) // 16
+    nv = (nvals + pre_lanes - 1) // pre_lanes
     nt = max([len(k) for k in order] or [0])
     np_ = max(len(p) for _, p, _ in per_lane)
     nl = max(len(q) for _, _, q in per_lane)
@@ -792,8 +794,8 @@ def compile_round(lanes, name, scratch_cap, lanes2=None):
     for t in range(16):
         pre = []
         for v in range(nv):
-            vi = t + 16 * v
-            if vi < nvals:
+            vi = t + pre_lanes * v
+            if t < pre_lanes and vi < nvals:
                 terms = list(order[vi]) + [(zero, 0)] * (nt - len(order[vi]))
                 pre.append((X_SCR + vi, terms))
             else:
@@ -914,6 +916,9 @@ def run_xround(xr, F, A, B):
 
 
 X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
+# programs whose pre-pass values live on lanes 0..11 only, so that they also
+# run in 12-lane teams (five per wave: k_gt_chunks, make_team12)
+PRE_LANES = {"MUL12F": 12}
 KARATSUBA_MIN = 4   # jobs of this many products use Karatsuba (when check_xround allows)
 # FE: the register file from register 2 on; ML: slots C..J during the Miller loop
 # FOLD: the GT fold kernels' compact team region (bn256_gt.hip): slots F, A, B,
@@ -961,7 +966,8 @@ def compile_all():
         if name in FUSED:
             X[name] = _compile_fused(name, ctx)
         else:
-            X[name] = [compile_round(r, f"{name}[{i}]", SCRATCH_CAP[ctx]) for i, r in enumerate(PROGRAMS[name])]
+            X[name] = [compile_round(r, f"{name}[{i}]", SCRATCH_CAP[ctx], pre_lanes=PRE_LANES.get(name, 16))
+                       for i, r in enumerate(PROGRAMS[name])]
     return X
 
 
