@@ -453,53 +453,83 @@ HG_DEV bool t12_is_one(const Team& T, int s) {
   return ((bal >> team_shift) & 0xffffull) == 0xffffull;
 }
 
-// ---------------------------------------------------------------- Fp6 helpers (redundant, per lane)
-HG_DEV void f6_inv_lane(Fp2& r0, Fp2& r1, Fp2& r2, const Fp2& c0, const Fp2& c1, const Fp2& c2) {
-  Fp2 t0, t1, t2, s, d;
-  f2_sqr(t0, c0);
-  f2_mul(s, c1, c2);
-  f2_mul_xi(s, s);
-  f2_sub(t0, t0, s);
-  f2_sqr(t1, c2);
-  f2_mul_xi(t1, t1);
-  f2_mul(s, c0, c1);
-  f2_sub(t1, t1, s);
-  f2_sqr(t2, c1);
-  f2_mul(s, c0, c2);
-  f2_sub(t2, t2, s);
-  f2_mul(d, c2, t1);
-  f2_mul(s, c1, t2);
-  f2_add(d, d, s);
-  f2_mul_xi(d, d);
-  f2_mul(s, c0, t0);
-  f2_add(d, d, s);
-  f2_inv(d, d);
-  f2_mul(r0, t0, d);
-  f2_mul(r1, t1, d);
-  f2_mul(r2, t2, d);
-}
-
 // slot s2 holds N = a conj(a) (an Fp6 element over tau = w^2: odd coefficients
-// zero); replaces it by N^-1. Every lane inverts N redundantly.
+// zero); replaces it by N^-1 = adj(N) / d (x/crypto gfP6.Invert:
+// t0 = c0^2 - xi c1 c2, t1 = xi c2^2 - c0 c1, t2 = c1^2 - c0 c2,
+// d = xi (c2 t1 + c1 t2) + c0 t0). The adjugate's three products and d's
+// three terms are split over lanes 0..2 with one instruction stream (lane j
+// computes term j; the odd, zero coefficients of s2 carry them between lanes),
+// so a lane runs 2 + 1 Fp2 products instead of 9; the Fp2 inversion of d (one
+// Bernstein-Yang Fp inversion) runs on every lane, and each lane finishes
+// its own element of N^-1 with one lazy sum of two products.
 HG_DEV void t12_inv_norm(const Team& T, int s2) {
-  Fp2 n0, n1, n2;
-  ld_f2(n0, slot(T, s2), 0);
-  ld_f2(n1, slot(T, s2), 2);
-  ld_f2(n2, slot(T, s2), 4);
-  Fp2 i0, i1, i2;
-  f6_inv_lane(i0, i1, i2, n0, n1, n2);
+  uint32_t* N = slot(T, s2);
+  Fp2 c0, c1, c2;
+  ld_f2(c0, N, 0);
+  ld_f2(c1, N, 2);
+  ld_f2(c2, N, 4);
+  const int j = T.tl < 3 ? T.tl : 2;
+  // t_j = alpha X^2 - beta Y Z with (X, alpha; Y, Z, beta) per j
+  Fp2 X, Y, Z, u, v, t;
+  f2_sel(X, j == 0, c0, j == 1 ? c2 : c1);
+  f2_sel(Y, j == 0, c1, c0);
+  f2_sel(Z, j == 1, c1, c2);
+  f2_sqr(u, X);
+  f2_mul(v, Y, Z);
+  Fp2 xu, xv;
+  f2_mul_xi(xu, u);
+  f2_mul_xi(xv, v);
+  f2_sel(u, j == 1, xu, u);
+  f2_sel(v, j == 0, xv, v);
+  f2_sub(t, u, v);
   team_sync();
-  {
-    // store N^-1 as an Fp12 with zero odd coefficients
-    int m = T.k >> 1;
-    Fp2 v;
-    f2_sel(v, m == 0, i0, (m == 1) ? i1 : i2);
-    Fp z, e;
-    fp_zero(z);
-    e = T.comp ? v.y : v.x;
-    fp_sel(e, (T.k & 1) != 0, z, e);
-    if (T.active) st_fp(slot(T, s2) + T.e * 10, e);
+  if (T.tl < 3) {  // odd coefficient 2j + 1 of s2
+    st_fp(N + (4 * j + 2) * 10, t.x);
+    st_fp(N + (4 * j + 3) * 10, t.y);
   }
+  team_sync();
+  Fp2 t0, t1, t2;
+  ld_f2(t0, N, 1);
+  ld_f2(t1, N, 3);
+  ld_f2(t2, N, 5);
+  // term j of d: c2 t1, c1 t2, c0 t0
+  Fp2 P, Q, w;
+  f2_sel(P, j == 0, c2, j == 1 ? c1 : c0);
+  f2_sel(Q, j == 0, t1, j == 1 ? t2 : t0);
+  f2_mul(w, P, Q);
+  team_sync();
+  if (T.tl < 3) {
+    st_fp(N + (4 * j + 2) * 10, w.x);
+    st_fp(N + (4 * j + 3) * 10, w.y);
+  }
+  team_sync();
+  Fp2 w0, w1, w2, d;
+  ld_f2(w0, N, 1);
+  ld_f2(w1, N, 3);
+  ld_f2(w2, N, 5);
+  f2_add(d, w0, w1);
+  f2_mul_xi(d, d);
+  f2_add(d, d, w2);
+  f2_inv(d, d);
+  // element e of N^-1: component comp of t_m d^-1 (m = k / 2), zero for odd k
+  const int m = T.k >> 1;
+  Fp2 tm;
+  f2_sel(tm, m == 0, t0, m == 1 ? t1 : t2);
+  // x (imag) = tm.x d.y + tm.y d.x; y (real) = tm.y d.y - tm.x d.x
+  Fp a1, b1, ntx;
+  fp_neg_loose(ntx, tm.x);
+  fp_sel(a1, T.comp != 0, tm.y, tm.x);
+  fp_sel(b1, T.comp != 0, ntx, tm.y);
+  Acc acc;
+  acc_zero(acc);
+  acc_mad(acc, a1, d.y);
+  acc_mad(acc, b1, d.x);
+  Fp e, z;
+  acc_reduce(e, acc);
+  fp_zero(z);
+  fp_sel(e, (T.k & 1) != 0, z, e);
+  team_sync();
+  if (T.active) st_fp(N + T.e * 10, e);
   team_sync();
 }
 
