@@ -604,6 +604,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="headline only (no single / full / pipelined lines)")
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight for the 'pipelined' line (1: skip)")
+    ap.add_argument("--pipeline-overlap", type=int, default=1,
+                    help="the pipelined line's contexts run their fold beside the pairing kernel (1) or before it (0)")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="requests in the CPU baseline's sample")
     args = ap.parse_args()
 
@@ -772,6 +774,8 @@ def main():
             # a verifier serving a continuous stream: batches in flight on several
             # HIP streams, one engine context (own workspaces) per stream
             engs = [eng] + [Engine(device=local_dev, flavor="go") for _ in range(args.pipeline - 1)]
+            for e in engs:
+                e.set_fold_overlap(bool(args.pipeline_overlap))
             for e in engs[1:]:
                 assert e.set_message(LIB_MESSAGE) == 0
                 assert not e.registry_load(head.reg).any()
@@ -792,6 +796,7 @@ def main():
                                   "note": "headline batch on each of the streams; throughput with batches overlapped"}
             for e in engs[1:]:
                 e.close()
+            eng.set_fold_overlap(True)
 
         extra["packet_intake"] = packet_intake(eng, head, n_reg, dev, stream, timer, args, world)
         extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)

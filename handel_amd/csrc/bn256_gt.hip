@@ -657,6 +657,11 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
   // SIMDs: the pairing wave (the step's critical path) wins the issue
   // arbitration, the fold's waves take the cycles it leaves
   if (kStore) __builtin_amdgcn_s_setprio(3);
+  // one pairing wave per SIMD: the kernel needs 233 VGPRs, which would let a
+  // second batch's pairing waves (two contexts in flight) share SIMDs and
+  // crowd the fold's workgroups out of the CU's LDS; marking v255 and one
+  // AGPR used makes its allocation exceed half of the 512-entry file
+  asm volatile("" ::: "v255", "a0");
   Team T = make_team(lds, kSigTeamWords);
   uint32_t* F = team_regs(T);
   const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
