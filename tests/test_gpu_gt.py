@@ -132,11 +132,16 @@ def test_gt_and_g2_paths_agree():
     16-key windows (HG_GT_LEVEL=2), over 8-key windows (1), the G2 point fold
     + two-pairing check (0, and HG_AGG_PATH=g2) — each in a child process."""
     outs = {}
+    # gt16c16 / gt16c5: chunks of 16 and 5 terms per fold team (HG_GT_CHUNK):
+    # a 12-lane team (k_gt_chunks) reads terms past 12 from the term list
     for name, env in (("gt16", {"HG_GT_LEVEL": "2"}), ("gt8", {"HG_GT_LEVEL": "1"}),
-                      ("g2", {"HG_GT_LEVEL": "0"}), ("g2env", {"HG_AGG_PATH": "g2"})):
+                      ("g2", {"HG_GT_LEVEL": "0"}), ("g2env", {"HG_AGG_PATH": "g2"}),
+                      ("gt16c16", {"HG_GT_LEVEL": "2", "HG_GT_CHUNK": "16"}),
+                      ("gt16c5", {"HG_GT_LEVEL": "2", "HG_GT_CHUNK": "5"})):
         outs[name] = _child(env)
-    assert [outs[k]["level"] for k in ("gt16", "gt8", "g2", "g2env")] == [2, 1, 0, 0]
-    assert outs["gt16"]["codes"] == outs["gt8"]["codes"] == outs["g2"]["codes"] == outs["g2env"]["codes"]
+    assert [outs[k]["level"] for k in ("gt16", "gt8", "g2", "g2env", "gt16c16", "gt16c5")] == [2, 1, 0, 0, 2, 2]
+    assert (outs["gt16"]["codes"] == outs["gt8"]["codes"] == outs["g2"]["codes"] == outs["g2env"]["codes"]
+            == outs["gt16c16"]["codes"] == outs["gt16c5"]["codes"])
     import bench
     from handel_amd.engine import Engine
 
