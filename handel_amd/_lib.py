@@ -106,6 +106,19 @@ SIGNATURES = {
     "hg_batcher_wait": (_I, [_P, _P, _P]),
     "hg_batcher_verify_aggregate": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
     "hg_batcher_stats": (_I, [_P, _P, _P]),
+    "hg_prepare_aggregate_level": (_I, [_P, _I]),
+    "hg_lane_create": (_I, [_P, _SZ, _SZ, _I, ctypes.POINTER(_P)]),
+    "hg_lane_destroy": (None, [_P]),
+    "hg_lane_stage": (_I, [_P, _SZ, _SZ, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "hg_lane_submit": (_I, [_P]),
+    "hg_lane_query": (_I, [_P]),
+    "hg_lane_wait": (_I, [_P]),
+    "hg_lane_codes": (ctypes.POINTER(ctypes.c_int32), [_P]),
+    "hg_service_config_init": (None, [_P]),
+    "hg_service_create": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_P)]),
+    "hg_service_create_echo": (_I, [ctypes.c_char_p, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_P)]),
+    "hg_service_destroy": (None, [_P]),
+    "hg_service_stats": (_I, [_P, _P, _P, _P]),
 }
 
 

@@ -19,9 +19,10 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libhandel_gpu.so")
 DIAG_LIB = os.path.join(OUT_DIR, "libhandel_gpu_diag.so")
-SOURCES = ["bn256_verify.hip", "bn256_pair.hip", "bn256_kernels.hip", "bn256_gt.hip", "hg_api.cpp", "hg_batcher.cpp", "hg_packets.hip"]
+SOURCES = ["bn256_verify.hip", "bn256_pair.hip", "bn256_kernels.hip", "bn256_gt.hip", "hg_api.cpp", "hg_batcher.cpp", "hg_packets.hip",
+           "hg_service.cpp"]
 HEADERS = ["bn256_fp.h", "bn256_curve.h", "bn256_team.h", "bn256_kernels.h", "bn256_constants.h",
-           "bn256_g2team.h", "bn256_g2sched.h", "bn256_pairing.h", "bn256_xprog.h", "bn256_xtab.h", "bn256_inv.h", "bn256_agg.h", "bn256_gt.h", "bn256_decode.h", "hg_packets.h"]
+           "bn256_g2team.h", "bn256_g2sched.h", "bn256_pairing.h", "bn256_xprog.h", "bn256_xtab.h", "bn256_inv.h", "bn256_agg.h", "bn256_gt.h", "bn256_decode.h", "hg_packets.h", "hg_shm.h"]
 ARCH = os.environ.get("HG_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
@@ -73,6 +74,28 @@ def build_library(force: bool = False, verbose: bool = True, diag: bool = False,
     return lib
 
 
+CLIENT_LIB = os.path.join(OUT_DIR, "libhandel_client.so")
+
+
+def build_client(force: bool = False, verbose: bool = True) -> str:
+    """libhandel_client.so: the verifier service's client side (hg_client.cpp,
+    include/handel_client.h), host compiler only — no HIP runtime, so client
+    processes never touch the GPU."""
+    srcs = [os.path.join(CSRC, "hg_client.cpp"), os.path.join(CSRC, "hg_shm.h"),
+            os.path.join(HERE, "..", "include", "handel_client.h"), os.path.join(HERE, "..", "include", "handel_gpu.h"),
+            os.path.abspath(__file__)]
+    if not force and os.path.exists(CLIENT_LIB) and os.path.getmtime(CLIENT_LIB) >= max(map(os.path.getmtime, srcs)):
+        return CLIENT_LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+    tmp = CLIENT_LIB + ".tmp"
+    cmd = ["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", "-Wextra", srcs[0], "-lpthread", "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(tmp, CLIENT_LIB)
+    return CLIENT_LIB
+
+
 ABI_THREADS = os.path.join(OUT_DIR, "abi_threads")
 
 
@@ -100,9 +123,8 @@ def build_proxy(verbose: bool = True) -> str:
     """tests/native/handel_proxy.c: the config-4 process-model proxy (forks
     the processes first, each dlopen()s the library: never linked here)."""
     src = os.path.join(HERE, "..", "tests", "native", "handel_proxy.c")
-    hdr = os.path.join(HERE, "..", "include", "handel_gpu.h")
-    if os.path.exists(HANDEL_PROXY) and os.path.getmtime(HANDEL_PROXY) >= max(os.path.getmtime(src),
-                                                                             os.path.getmtime(hdr)):
+    hdrs = [os.path.join(HERE, "..", "include", h) for h in ("handel_gpu.h", "handel_client.h")]
+    if os.path.exists(HANDEL_PROXY) and os.path.getmtime(HANDEL_PROXY) >= max(map(os.path.getmtime, [src, *hdrs])):
         return HANDEL_PROXY
     os.makedirs(OUT_DIR, exist_ok=True)
     cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-I", os.path.join(HERE, "..", "include"), src, "-ldl",
@@ -116,5 +138,6 @@ def build_proxy(verbose: bool = True) -> str:
 if __name__ == "__main__":
     print(build_library(force="--force" in sys.argv, diag="--diag" in sys.argv))
     if "--diag" not in sys.argv:
+        print(build_client())
         print(build_native_tests())
         print(build_proxy())

@@ -142,6 +142,72 @@ struct DevBuf {
   }
 };
 
+// Device workspaces of one in-flight submission: the context's own set (every
+// hg_* entry point, ordered by the context's submission chain) and one set
+// per service lane (hg_lane below), so several lanes' batches run at once
+// over the same registry and GT tables.
+struct Ws {
+  DevBuf<PointG2> pts2;
+  DevBuf<PointG1> pts1;
+  DevBuf<CheckIn> checks;
+  DevBuf<int32_t> codes_b, codes_c;
+  DevBuf<int> order;       // aggregation schedule (k_agg_order)
+  DevBuf<uint8_t> agg_ws;  // per-request fold results (k_aggregate -> k_agg_finish)
+  // GT fold workspaces
+  DevBuf<GtReq> gt_plan;
+  DevBuf<GtHdr> gt_hdr;
+  DevBuf<uint32_t> gt_terms;
+  DevBuf<int2> gt_ord;
+  DevBuf<int> gt_multi;
+  DevBuf<Gt> gt_partial, gt_y;
+  // the fold runs on a side stream beside the pairing kernel (GT path): the
+  // FE values of the batch land in gt_fe, k_gt_compare joins the two
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  DevBuf<Gt> gt_fe;
+  void release() {
+    pts2.release();
+    pts1.release();
+    checks.release();
+    codes_b.release();
+    codes_c.release();
+    order.release();
+    agg_ws.release();
+    gt_plan.release();
+    gt_hdr.release();
+    gt_terms.release();
+    gt_ord.release();
+    gt_multi.release();
+    gt_partial.release();
+    gt_y.release();
+    gt_fe.release();
+    if (side) (void)hipStreamDestroy(side);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    side = nullptr;
+    ev_fork = ev_join = nullptr;
+  }
+  size_t bytes() const {
+    return pts2.cap * sizeof(PointG2) + pts1.cap * sizeof(PointG1) + checks.cap * sizeof(CheckIn) +
+           (codes_b.cap + codes_c.cap) * sizeof(int32_t) + order.cap * sizeof(int) + agg_ws.cap +
+           gt_plan.cap * sizeof(GtReq) + gt_hdr.cap * sizeof(GtHdr) + gt_terms.cap * sizeof(uint32_t) +
+           gt_ord.cap * sizeof(int2) + gt_multi.cap * sizeof(int) + (gt_partial.cap + gt_y.cap + gt_fe.cap) * sizeof(Gt);
+  }
+};
+
+// The per-message part of the context: hashedMessage and the GT tables
+// e(H, .) of the registry. The context keeps the current message's set and
+// the previous one (hg_set_message switches between the two without a
+// rebuild, so interleaved messages keep their tables).
+struct TableSet {
+  std::vector<uint8_t> msg;
+  bool has_msg = false, hash_eof = false;
+  PointG1* d_h = nullptr;
+  DevBuf<Gt> gt_key, gt_w8, gt_win, gt_blk;
+  int gt_level = 0;
+  size_t gt_requests = 0;
+};
+
 }  // namespace
 
 struct hg_ctx {
@@ -167,15 +233,12 @@ struct hg_ctx {
   std::vector<int> block_base = std::vector<int>(24, 0);
   int block_levels = 0;
   // workspaces
+  Ws ws;
   DevBuf<uint8_t> bytes_a, bytes_b;
-  DevBuf<PointG2> pts2;
-  DevBuf<PointG1> pts1, pts1b;
-  DevBuf<CheckIn> checks;
-  DevBuf<int32_t> codes_a, codes_b, codes_c;
+  DevBuf<PointG1> pts1b;
+  DevBuf<int32_t> codes_a;
   DevBuf<hg_request> reqs;
   DevBuf<hg_packet> pkts;  // hg_parse_packets staging
-  DevBuf<int> order;       // aggregation schedule (k_agg_order)
-  DevBuf<uint8_t> agg_ws;  // per-request fold results (k_aggregate -> k_agg_finish)
   DevBuf<uint64_t> words;
   // GT path of aggregate verification (bn256_gt.hip): e(H, pk_i), window
   // subset products and block products, valid for the current message and
@@ -202,35 +265,61 @@ struct hg_ctx {
   DevBuf<int> sub_count;
   DevBuf<Gt> gt_key, gt_w8, gt_win, gt_blk;  // gt_w8: 8-key windows, gt_win: 16-key windows
   GtBlockIndex gt_bi{};
-  // GT fold workspaces
-  DevBuf<GtReq> gt_plan;
-  DevBuf<GtHdr> gt_hdr;
-  DevBuf<uint32_t> gt_terms;
-  DevBuf<int2> gt_ord;
-  DevBuf<int> gt_multi;
-  DevBuf<Gt> gt_partial, gt_y;
-  // the fold runs on a side stream beside the pairing kernel (GT path): the
-  // FE values of the batch land in gt_fe, k_gt_compare joins the two
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  DevBuf<Gt> gt_fe;
+  // the previous message's hashedMessage and tables (swapped with the fields
+  // above by set_message_locked; see TableSet)
+  TableSet alt;
+  // the cap a failed device allocation set (gt_cap also follows the table
+  // budget; hg_set_table_budget re-derives gt_cap from this)
+  int oom_cap = 2;
   bool overlap = true;  // hg_set_fold_overlap; HG_GT_OVERLAP=0 gives new contexts false
   // submission order across streams: the event recorded after the last
   // submission and the stream it ran on (the workspaces above are shared)
   hipEvent_t last_ev = nullptr;
   hipStream_t last_s = nullptr;
+  // service lanes (hg_lane): batches in flight on their own workspaces and
+  // streams; every context submission first waits for their last batches
+  // (they read the registry, H and the tables a submission may rewrite)
+  std::vector<hg_lane*> lanes;
   // optional per-phase timing (bench roofline), see hg_timing_read_phase
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events[HG_NUM_PHASES];
+};
+
+// One service lane (hg_service.cpp): one batch at a time in flight on its own
+// stream and workspaces, beside the other lanes' batches. The batch's inputs
+// (requests | signatures | bitset words) are staged in pinned host memory and
+// go to the device in ONE copy; the codes come back the same way.
+struct hg_lane {
+  hg_ctx* c = nullptr;
+  Ws ws;
+  hipStream_t s = nullptr;
+  hipEvent_t done = nullptr;
+  bool recorded = false;  // `done` marks the lane's last batch
+  bool overlap = true;    // the fold beside the pairing kernel (on ws.side)
+  size_t max_batch = 0, max_words = 0;
+  uint8_t* h_in = nullptr;     // pinned staging
+  int32_t* h_codes = nullptr;  // pinned
+  DevBuf<uint8_t> d_in;
+  DevBuf<int32_t> d_codes;
+  size_t n = 0, nwords = 0, off_sigs = 0, off_words = 0, in_bytes = 0;
 };
 
 // ---------------------------------------------------------------- submission order
 // Every device submission of a context runs between begin() and end(): a
 // submission on another stream than the previous one first waits for the
 // previous one's event, so two submissions never use the shared workspaces
-// (or the registry tables and H) at the same time.
+// (or the registry tables and H) at the same time. Service lanes keep their
+// own workspaces; a context submission waits for each lane's last batch.
 static hipError_t begin(hg_ctx* c, hipStream_t s) {
-  if (c->last_ev && c->last_s != s) return hipStreamWaitEvent(s, c->last_ev, 0);
+  if (c->last_ev && c->last_s != s) {
+    hipError_t e = hipStreamWaitEvent(s, c->last_ev, 0);
+    if (e != hipSuccess) return e;
+  }
+  for (hg_lane* l : c->lanes) {
+    if (!l->recorded) continue;
+    hipError_t e = hipStreamWaitEvent(s, l->done, 0);
+    if (e != hipSuccess) return e;
+  }
   return hipSuccess;
 }
 static hipError_t end(hg_ctx* c, hipStream_t s) {
@@ -316,44 +405,38 @@ static int check_launch(hg_ctx* c) {
   return HG_OK;
 }
 
+static void release_tables(TableSet& t) {
+  t.gt_key.release();
+  t.gt_w8.release();
+  t.gt_win.release();
+  t.gt_blk.release();
+  t.gt_level = 0;
+}
+
 static void release_all(hg_ctx* c) {
   c->reg.release();
   c->blocks.release();
   c->wsum.release();
   c->bytes_a.release();
   c->bytes_b.release();
-  c->pts2.release();
-  c->pts1.release();
   c->pts1b.release();
-  c->checks.release();
   c->codes_a.release();
-  c->codes_b.release();
-  c->codes_c.release();
   c->reqs.release();
-  c->order.release();
-  c->agg_ws.release();
   c->words.release();
   c->gt_key.release();
   c->gt_w8.release();
   c->gt_win.release();
   c->gt_blk.release();
-  c->gt_plan.release();
-  c->gt_hdr.release();
-  c->gt_terms.release();
-  c->gt_ord.release();
-  c->gt_multi.release();
-  c->gt_partial.release();
-  c->gt_y.release();
-  c->gt_fe.release();
   c->gt_level = 0;
-  if (c->side) (void)hipStreamDestroy(c->side);
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  release_tables(c->alt);
+  if (c->alt.d_h) (void)hipFree(c->alt.d_h);
+  c->alt.d_h = nullptr;
+  c->alt.has_msg = false;
+  c->ws.release();
   if (c->ev_sub) (void)hipEventDestroy(c->ev_sub);
   c->sub_count.release();
   c->sub_pending = false;
-  c->side = nullptr;
-  c->ev_fork = c->ev_join = c->ev_sub = nullptr;
+  c->ev_sub = nullptr;
   for (auto& ph : c->events) {
     for (auto& pr : ph) {
       (void)hipEventDestroy(pr.first);
@@ -373,16 +456,47 @@ static void release_all(hg_ctx* c) {
   c->stream = nullptr;
 }
 
-// hashedMessage into d_h (the caller holds the lock); HG_OK or HG_ERR_HASH_EOF
+// exchanges the context's current message part with the cached one
+static void swap_tables(hg_ctx* c) {
+  TableSet& t = c->alt;
+  std::swap(c->msg, t.msg);
+  std::swap(c->has_msg, t.has_msg);
+  std::swap(c->hash_eof, t.hash_eof);
+  std::swap(c->d_h, t.d_h);
+  std::swap(c->gt_key, t.gt_key);
+  std::swap(c->gt_w8, t.gt_w8);
+  std::swap(c->gt_win, t.gt_win);
+  std::swap(c->gt_blk, t.gt_blk);
+  std::swap(c->gt_level, t.gt_level);
+  std::swap(c->gt_requests, t.gt_requests);
+}
+
+static bool same_msg(const std::vector<uint8_t>& m, const uint8_t* msg, size_t len) {
+  return m.size() == len && (len == 0 || memcmp(m.data(), msg, len) == 0);
+}
+
+// hashedMessage into d_h (the caller holds the lock); HG_OK or HG_ERR_HASH_EOF.
+// The context keeps two messages (bn256/go/bn256.go:210-218: H and with it
+// every GT table is fixed per message): the current one and the previous one.
+// Switching back to the previous message swaps the two sets and keeps its
+// tables; a third message takes over the older set's buffers (level 0, its
+// tables rebuilt on demand). The hash and any later rebuild run in
+// submission order, after every submission that still reads the old set.
 static int set_message_locked(hg_ctx* c, const uint8_t* msg, size_t len) {
   HG_CHECK(c, hipSetDevice(c->device));
-  if (c->has_msg && c->msg.size() == len && (len == 0 || memcmp(c->msg.data(), msg, len) == 0))
+  if (c->has_msg && same_msg(c->msg, msg, len)) return c->hash_eof ? HG_ERR_HASH_EOF : HG_OK;
+  if (c->alt.has_msg && same_msg(c->alt.msg, msg, len)) {
+    swap_tables(c);
     return c->hash_eof ? HG_ERR_HASH_EOF : HG_OK;
+  }
+  // the current set becomes the cached one; the new message takes the other
+  if (c->has_msg) swap_tables(c);
+  if (!c->d_h) HG_CHECK(c, hipMalloc(&c->d_h, sizeof(PointG1)));
   uint8_t d[32];
   sha256(msg, len, d);
   uint32_t k[8];
   c->has_msg = false;
-  c->gt_level = 0;  // the GT tables are e(H, .) of the previous message
+  c->gt_level = 0;  // these buffers hold e(H, .) of an evicted message
   c->gt_requests = 0;
   c->msg.assign(msg, msg + len);
   c->hash_eof = !hash_scalar(d, k);
@@ -408,13 +522,13 @@ static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uin
     c->err = "hg_set_message was not called";
     return HG_ERR_ARG;
   }
-  HG_CHECK(c, c->checks.ensure(n));
+  HG_CHECK(c, c->ws.checks.ensure(n));
   Submission sub(c, s);
   HG_CHECK(c, sub.start());
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
-  launch_decode_checks(d_pks, d_sigs, (int)n, c->flavor, c->checks.p, d_codes, s);
+  launch_decode_checks(d_pks, d_sigs, (int)n, c->flavor, c->ws.checks.p, d_codes, s);
   if (c->hash_eof) k_fill_codes<<<nb(n), 256, 0, s>>>(d_codes, (int)n, HG_OK, HG_ERR_HASH_EOF);
-  else timed_verify(c, c->checks.p, (int)n, d_codes, s);
+  else timed_verify(c, c->ws.checks.p, (int)n, d_codes, s);
   all.stop();
   int rc = check_launch(c);
   if (rc) return rc;
@@ -426,14 +540,14 @@ static int verify_batch_host_locked(hg_ctx* c, const uint8_t* pks, const uint8_t
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 128));
   HG_CHECK(c, c->bytes_b.ensure(n * 64));
-  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, c->ws.codes_c.ensure(n));
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, pks, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
-  int rc = verify_batch_device_locked(c, c->bytes_a.p, c->bytes_b.p, n, c->codes_c.p, c->stream);
+  int rc = verify_batch_device_locked(c, c->bytes_a.p, c->bytes_b.p, n, c->ws.codes_c.p, c->stream);
   if (rc) return rc;
-  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->ws.codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
@@ -470,7 +584,8 @@ static void level_codes(hg_ctx* c, const hg_request* reqs, size_t n, std::vector
 static constexpr size_t kGtMaxRegistry = 16384;
 static constexpr size_t kGtLevel1Requests = 16384;
 static constexpr size_t kGtLevel2Requests = (size_t)1 << 20;
-static constexpr int kNoMem = -1;  // internal: an allocation of the GT path failed (or is over budget)
+static constexpr int kNoMem = -1;       // internal: an allocation of the GT path failed
+static constexpr int kOverBudget = -2;  // internal: a table level exceeds hg_set_table_budget
 static int gt_forced_level() {
   static const int lvl = [] {
     const char* p = getenv("HG_AGG_PATH");
@@ -532,13 +647,25 @@ static size_t gt_table_bytes(const hg_ctx* c, int level) {
   return b;
 }
 
-// builds the tables up to `level` on stream s (inside a submission); kNoMem
-// before any launch of the level that could not be held
+static size_t alt_table_bytes(const hg_ctx* c) {
+  const TableSet& t = c->alt;
+  return (t.gt_key.cap + t.gt_w8.cap + t.gt_win.cap + t.gt_blk.cap) * sizeof(Gt);
+}
+// frees the cached message's tables (its hash stays); false if it held none
+static bool drop_alt_tables(hg_ctx* c) {
+  if (alt_table_bytes(c) == 0) return false;
+  release_tables(c->alt);
+  return true;
+}
+
+// builds the tables up to `level` on stream s (inside a submission); kNoMem /
+// kOverBudget before any launch of the level that could not be held. The
+// budget covers both messages' tables.
 static int build_gt_locked(hg_ctx* c, hipStream_t s, int level) {
   const int n = (int)c->nreg;
   const int nwin8 = (n + 7) / 8, nwin16 = (n + 15) / 16;
   if (c->gt_level < 1 && level >= 1) {
-    if (gt_table_bytes(c, 1) > c->table_budget) return kNoMem;
+    if (gt_table_bytes(c, 1) + alt_table_bytes(c) > c->table_budget) return kOverBudget;
     int cnt[24] = {0};
     const size_t total = gt_block_count(c, cnt);
     int base = 0;
@@ -560,7 +687,7 @@ static int build_gt_locked(hg_ctx* c, hipStream_t s, int level) {
     c->gt_level = 1;
   }
   if (c->gt_level < 2 && level >= 2) {
-    if (gt_table_bytes(c, 2) > c->table_budget) return kNoMem;
+    if (gt_table_bytes(c, 2) + alt_table_bytes(c) > c->table_budget) return kOverBudget;
     HG_GT_ALLOC(c, c->gt_win.ensure((size_t)nwin16 * 65536));
     launch_gt_windows16(c->gt_w8.p, nwin8, c->gt_win.p, nwin16, s);
     int rc = check_launch(c);
@@ -570,10 +697,12 @@ static int build_gt_locked(hg_ctx* c, hipStream_t s, int level) {
   return HG_OK;
 }
 
-// caps the context's table level at `cap` and frees the tables above it
-static void gt_lower_cap(hg_ctx* c, int cap) {
+// caps the context's table level at `cap` and frees the tables above it; an
+// out-of-memory cap also holds across later budget changes (oom_cap)
+static void gt_lower_cap(hg_ctx* c, int cap, bool oom) {
   if (cap < 0) cap = 0;
   if (cap < c->gt_cap) c->gt_cap = cap;
+  if (oom && cap < c->oom_cap) c->oom_cap = cap;
   if (c->gt_cap < 2) c->gt_win.release();
   if (c->gt_cap < 1) {
     c->gt_key.release();
@@ -581,6 +710,22 @@ static void gt_lower_cap(hg_ctx* c, int cap) {
     c->gt_blk.release();
   }
   if (c->gt_level > c->gt_cap) c->gt_level = c->gt_cap;
+}
+
+// builds up to `level` (lowering it to what fits: the cached message's tables
+// go first, then the cap); HG_OK with `level` = what was built
+static int build_fitting_locked(hg_ctx* c, hipStream_t s, int& level) {
+  while (level > c->gt_level) {
+    int rc = build_gt_locked(c, s, level);
+    if (rc == kNoMem || rc == kOverBudget) {
+      if (drop_alt_tables(c)) continue;
+      gt_lower_cap(c, c->gt_level < level ? c->gt_level : level - 1, rc == kNoMem);
+      level = level < c->gt_cap ? level : c->gt_cap;
+      continue;
+    }
+    if (rc) return rc;
+  }
+  return HG_OK;
 }
 
 // the table level an aggregate submission of n requests runs at (counting
@@ -632,23 +777,23 @@ static FoldCaps fold_caps_worst(const hg_ctx* c, size_t n) {
   all.chunks = one.chunks * n;
   return all;
 }
-static int ensure_gt_fold(hg_ctx* c, size_t n, const FoldCaps& caps, GtWork& w) {
+static int ensure_gt_fold(hg_ctx* c, Ws& ws, size_t n, const FoldCaps& caps, GtWork& w) {
   static const int grid = env_int("HG_GT_GRID", 4096, 64, 65536);
   if (caps.chunks > (size_t)INT32_MAX || caps.terms > (size_t)INT32_MAX) return kNoMem;
-  HG_GT_ALLOC(c, c->gt_plan.ensure(n));
-  HG_GT_ALLOC(c, c->gt_hdr.ensure(1));
-  HG_GT_ALLOC(c, c->gt_terms.ensure(caps.terms));
-  HG_GT_ALLOC(c, c->gt_ord.ensure(caps.chunks));
-  HG_GT_ALLOC(c, c->gt_multi.ensure(2 * n));
-  HG_GT_ALLOC(c, c->gt_partial.ensure(caps.chunks));
-  HG_GT_ALLOC(c, c->gt_y.ensure(n));
-  w.plan = c->gt_plan.p;
-  w.hdr = c->gt_hdr.p;
-  w.terms = c->gt_terms.p;
-  w.ord = c->gt_ord.p;
+  HG_GT_ALLOC(c, ws.gt_plan.ensure(n));
+  HG_GT_ALLOC(c, ws.gt_hdr.ensure(1));
+  HG_GT_ALLOC(c, ws.gt_terms.ensure(caps.terms));
+  HG_GT_ALLOC(c, ws.gt_ord.ensure(caps.chunks));
+  HG_GT_ALLOC(c, ws.gt_multi.ensure(2 * n));
+  HG_GT_ALLOC(c, ws.gt_partial.ensure(caps.chunks));
+  HG_GT_ALLOC(c, ws.gt_y.ensure(n));
+  w.plan = ws.gt_plan.p;
+  w.hdr = ws.gt_hdr.p;
+  w.terms = ws.gt_terms.p;
+  w.ord = ws.gt_ord.p;
   w.cap = (int)caps.chunks;
-  w.multi = c->gt_multi.p;
-  w.partial = c->gt_partial.p;
+  w.multi = ws.gt_multi.p;
+  w.partial = ws.gt_partial.p;
   w.chunk_grid = grid;
   w.chunk = gt_chunk();
   return HG_OK;
@@ -658,21 +803,19 @@ static int ensure_gt_fold(hg_ctx* c, size_t n, const FoldCaps& caps, GtWork& w) 
 // on stream s). Lowers `level` for what the device cannot hold: tables that do
 // not fit cap the context (tables never get smaller for this registry), fold
 // workspaces that do not fit send this submission to the G2 fold only.
-static int gt_acquire(hg_ctx* c, hipStream_t s, size_t n, const FoldCaps& caps, int& level, GtWork& w) {
-  while (level > 0) {
-    int rc = c->gt_level < level ? build_gt_locked(c, s, level) : HG_OK;
-    if (rc == kNoMem) {
-      gt_lower_cap(c, c->gt_level < level ? c->gt_level : level - 1);
-      level = level < c->gt_cap ? level : c->gt_cap;
-      continue;
-    }
+// may_build = false (service lanes): run at the built level at most; builds
+// happen between batches, with the lanes drained (hg_lane_build_level)
+static int gt_acquire(hg_ctx* c, Ws& ws, hipStream_t s, size_t n, const FoldCaps& caps, int& level, GtWork& w,
+                      bool may_build = true) {
+  if (!may_build && level > c->gt_level) level = c->gt_level;
+  if (level > 0 && c->gt_level < level) {
+    int rc = build_fitting_locked(c, s, level);
     if (rc) return rc;
-    rc = ensure_gt_fold(c, n, caps, w);
-    if (rc == kNoMem) {
-      level = 0;
-      break;
-    }
-    return rc;
+  }
+  if (level > 0) {
+    int rc = ensure_gt_fold(c, ws, n, caps, w);
+    if (rc == kNoMem) level = 0;
+    else if (rc) return rc;
   }
   return HG_OK;
 }
@@ -685,11 +828,11 @@ static bool gt_overlap() {
   static const bool on = env_int("HG_GT_OVERLAP", 1, 0, 1) != 0;
   return on;
 }
-static hipError_t ensure_side(hg_ctx* c) {
+static hipError_t ensure_side(Ws& ws) {
   hipError_t e = hipSuccess;
-  if (!c->side) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-  if (e == hipSuccess && !c->ev_fork) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
-  if (e == hipSuccess && !c->ev_join) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+  if (!ws.side) e = hipStreamCreateWithFlags(&ws.side, hipStreamNonBlocking);
+  if (e == hipSuccess && !ws.ev_fork) e = hipEventCreateWithFlags(&ws.ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess && !ws.ev_join) e = hipEventCreateWithFlags(&ws.ev_join, hipEventDisableTiming);
   return e;
 }
 
@@ -707,121 +850,126 @@ __global__ void k_level_codes(const hg_request* r, int n, uint32_t nreg, int32_t
 // capacities (nullptr: bounded by the registry size).
 // d_bits (nullable): the verdict bitset of the codes, written in the same
 // submission (hg_pack_verdicts_device's layout)
+// lane (nullable): a service lane's submission — its own workspaces, outside
+// the context's submission chain, never building tables.
 static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
                                    const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_agg, int32_t* d_lvl,
                                    bool verify, hipStream_t s, const FoldCaps* caps = nullptr,
-                                   uint8_t* d_bits = nullptr) {
+                                   uint8_t* d_bits = nullptr, hg_lane* lane = nullptr) {
   if (verify && !c->has_msg) {
     c->err = "hg_set_message was not called";
     return HG_ERR_ARG;
   }
+  Ws& ws = lane ? lane->ws : c->ws;
   Submission sub(c, s);
-  HG_CHECK(c, sub.start());
+  if (!lane) HG_CHECK(c, sub.start());
   // GT path: the verdict needs no aggregate key in G2; the G2 fold still runs
   // when the caller wants the aggregate keys' marshals
   int level = verify ? gt_submission_level(c, n) : 0;
   GtWork gw{};
   if (level > 0) {
     const FoldCaps fc = caps ? *caps : fold_caps_worst(c, n);
-    int rc = gt_acquire(c, s, n, fc, level, gw);
+    int rc = gt_acquire(c, ws, s, n, fc, level, gw, lane == nullptr);
     if (rc) return rc;
   }
   const bool use_gt = level > 0;
   const bool g2_fold = !use_gt || d_agg;
   if (g2_fold) {
-    HG_CHECK(c, c->checks.ensure(n));
-    HG_CHECK(c, c->order.ensure(n));
-    HG_CHECK(c, c->agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
+    HG_CHECK(c, ws.checks.ensure(n));
+    HG_CHECK(c, ws.order.ensure(n));
+    HG_CHECK(c, ws.agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes()));
   }
-  if (d_agg) HG_CHECK(c, c->pts2.ensure(n));
-  if (!d_lvl) HG_CHECK(c, c->codes_c.ensure(n));
+  if (d_agg) HG_CHECK(c, ws.pts2.ensure(n));
+  if (!d_lvl) HG_CHECK(c, ws.codes_c.ensure(n));
   if (verify) {
-    HG_CHECK(c, c->pts1.ensure(n));
-    HG_CHECK(c, c->codes_b.ensure(n));
+    HG_CHECK(c, ws.pts1.ensure(n));
+    HG_CHECK(c, ws.codes_b.ensure(n));
   }
   gw.win_bits = level == 2 ? 16 : 8;
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
   if (use_gt && !g2_fold) {
     // GT path, verdicts only: level check, signature decode and the fold's
     // counters in one launch, then the fold and the check on d_codes
-    const bool overlap = c->overlap;
+    const bool overlap = lane ? lane->overlap : c->overlap;
     if (overlap) {
-      HG_CHECK(c, ensure_side(c));
-      HG_CHECK(c, c->gt_fe.ensure(n));
+      HG_CHECK(c, ensure_side(ws));
+      HG_CHECK(c, ws.gt_fe.ensure(n));
     }
     if (overlap) {
       // s:    pairing (decodes its signatures) ............ -> wait -> compare
       // side: wait -> prologue (codes, counters), plan, chunks, combine -> join
-      HG_CHECK(c, hipEventRecord(c->ev_fork, s));
+      HG_CHECK(c, hipEventRecord(ws.ev_fork, s));
       PhaseTimer t(c, HG_PHASE_VERIFY, s);
-      launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, c->gt_fe.p, s);
+      launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s);
       t.stop();
-      HG_CHECK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, c->pts1.p, d_codes, (int*)gw.hdr,
-                          (int)(sizeof(GtHdr) / sizeof(int)), c->side);
-      PhaseTimer fold(c, HG_PHASE_AGGREGATE, c->side);
+      HG_CHECK(c, hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
+      launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, ws.pts1.p, d_codes, (int*)gw.hdr,
+                          (int)(sizeof(GtHdr) / sizeof(int)), ws.side);
+      PhaseTimer fold(c, HG_PHASE_AGGREGATE, ws.side);
       launch_gt_fold(d_reqs, (int)n, d_words, d_codes, (int)c->nreg, c->block_levels,
-                     level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, false, c->side);
+                     level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, ws.gt_y.p, false, ws.side);
       fold.stop();
-      HG_CHECK(c, hipEventRecord(c->ev_join, c->side));
-      HG_CHECK(c, hipStreamWaitEvent(s, c->ev_join, 0));
-      if (d_bits) launch_gt_compare_bits(c->gt_fe.p, c->gt_y.p, (int)n, d_codes, d_bits, s);
-      else launch_gt_compare(c->gt_fe.p, c->gt_y.p, (int)n, d_codes, s);
+      HG_CHECK(c, hipEventRecord(ws.ev_join, ws.side));
+      HG_CHECK(c, hipStreamWaitEvent(s, ws.ev_join, 0));
+      if (d_bits) launch_gt_compare_bits(ws.gt_fe.p, ws.gt_y.p, (int)n, d_codes, d_bits, s);
+      else launch_gt_compare(ws.gt_fe.p, ws.gt_y.p, (int)n, d_codes, s);
       all.stop();
       int rc = check_launch(c);
       if (rc) return rc;
-      HG_CHECK(c, sub.finish());
+      if (!lane) HG_CHECK(c, sub.finish());
       return HG_OK;
     }
-    launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, c->pts1.p, d_codes, (int*)gw.hdr,
+    launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, ws.pts1.p, d_codes, (int*)gw.hdr,
                         (int)(sizeof(GtHdr) / sizeof(int)), s);
     PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
     launch_gt_fold(d_reqs, (int)n, d_words, d_codes, (int)c->nreg, c->block_levels,
-                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, false, s);
+                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, ws.gt_y.p, false, s);
     fold.stop();
     PhaseTimer t(c, HG_PHASE_VERIFY, s);
-    launch_verify_sig(c->pts1.p, (int)n, c->d_lines, c->gt_y.p, d_codes, s);
+    launch_verify_sig(ws.pts1.p, (int)n, c->d_lines, ws.gt_y.p, d_codes, s);
     t.stop();
     if (d_bits) launch_pack_verdicts(d_codes, (int)n, d_bits, s);
     all.stop();
     int rc = check_launch(c);
     if (rc) return rc;
-    HG_CHECK(c, sub.finish());
+    if (!lane) HG_CHECK(c, sub.finish());
     return HG_OK;
   }
   if (!d_lvl) {
-    d_lvl = c->codes_c.p;
+    d_lvl = ws.codes_c.p;
     k_level_codes<<<nb(n), 256, 0, s>>>(d_reqs, (int)n, (uint32_t)c->nreg, d_lvl);
   }
   PhaseTimer fold(c, HG_PHASE_AGGREGATE, s);
   if (g2_fold)
     launch_aggregate(c->wsum.p, (int)c->nreg, c->blocks.p, c->block_base.data(), c->block_levels, d_reqs, (int)n,
-                     d_words, c->order.p, c->agg_ws.p, c->checks.p, d_lvl, s);
+                     d_words, ws.order.p, ws.agg_ws.p, ws.checks.p, d_lvl, s);
   if (use_gt)
     launch_gt_fold(d_reqs, (int)n, d_words, d_lvl, (int)c->nreg, c->block_levels,
-                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, c->gt_y.p, true, s);
+                   level == 2 ? c->gt_win.p : c->gt_w8.p, c->gt_blk.p, c->gt_bi, gw, ws.gt_y.p, true, s);
   fold.stop();
   if (d_agg) {
-    launch_extract_pk(c->checks.p, (int)n, c->pts2.p, s);
-    launch_encode_g2(c->pts2.p, (int)n, d_agg, s);
+    launch_extract_pk(ws.checks.p, (int)n, ws.pts2.p, s);
+    launch_encode_g2(ws.pts2.p, (int)n, d_agg, s);
   }
   if (verify) {
-    launch_decode_g1(d_sigs, (int)n, c->flavor, c->pts1.p, c->codes_b.p, s);
-    k_agg_codes<<<nb(n), 256, 0, s>>>(c->codes_b.p, d_lvl, c->hash_eof ? 1 : 0, (int)n, d_codes);
+    launch_decode_g1(d_sigs, (int)n, c->flavor, ws.pts1.p, ws.codes_b.p, s);
+    k_agg_codes<<<nb(n), 256, 0, s>>>(ws.codes_b.p, d_lvl, c->hash_eof ? 1 : 0, (int)n, d_codes);
     if (use_gt) {
       PhaseTimer t(c, HG_PHASE_VERIFY, s);
-      launch_verify_sig(c->pts1.p, (int)n, c->d_lines, c->gt_y.p, d_codes, s);
+      launch_verify_sig(ws.pts1.p, (int)n, c->d_lines, ws.gt_y.p, d_codes, s);
       t.stop();
     } else if (!c->hash_eof) {
-      launch_sig_into_checks(c->pts1.p, (int)n, c->checks.p, s);
-      timed_verify(c, c->checks.p, (int)n, d_codes, s);
+      launch_sig_into_checks(ws.pts1.p, (int)n, ws.checks.p, s);
+      PhaseTimer t(c, HG_PHASE_VERIFY, s);
+      launch_verify(ws.checks.p, (int)n, c->d_lines, c->d_h, d_codes, s);
+      t.stop();
     }
   }
   if (d_bits) launch_pack_verdicts(d_codes, (int)n, d_bits, s);
   all.stop();
   int rc = check_launch(c);
   if (rc) return rc;
-  HG_CHECK(c, sub.finish());
+  if (!lane) HG_CHECK(c, sub.finish());
   return HG_OK;
 }
 
@@ -842,7 +990,7 @@ static int aggregate_host_locked(hg_ctx* c, const hg_request* reqs, size_t n, co
   HG_CHECK(c, c->reqs.ensure(n));
   HG_CHECK(c, c->words.ensure(nwords ? nwords : 1));
   HG_CHECK(c, c->codes_a.ensure(n));
-  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, c->ws.codes_c.ensure(n));
   uint8_t* d_agg = nullptr;
   if (agg_out) {
     HG_CHECK(c, c->bytes_a.ensure(n * 128));
@@ -853,13 +1001,13 @@ static int aggregate_host_locked(hg_ctx* c, const hg_request* reqs, size_t n, co
   HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->reqs.p, reqs, n * sizeof(hg_request), hipMemcpyHostToDevice, c->stream));
   if (nwords) HG_CHECK(c, hipMemcpyAsync(c->words.p, words, nwords * 8, hipMemcpyHostToDevice, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(c->codes_c.p, lvl.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(c->ws.codes_c.p, lvl.data(), n * 4, hipMemcpyHostToDevice, c->stream));
   if (verify) HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, sigs, n * 64, hipMemcpyHostToDevice, c->stream));
   int rc = aggregate_device_locked(c, c->reqs.p, n, c->words.p, verify ? c->bytes_b.p : nullptr, c->codes_a.p, d_agg,
-                                   c->codes_c.p, verify, c->stream, &caps);
+                                   c->ws.codes_c.p, verify, c->stream, &caps);
   if (rc) return rc;
   if (agg_out) HG_CHECK(c, hipMemcpyAsync(agg_out, d_agg, n * 128, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(codes, verify ? c->codes_a.p : c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, verify ? c->codes_a.p : c->ws.codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   if (agg_out) {
@@ -880,12 +1028,12 @@ static int sign_locked(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* 
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 64));
   HG_CHECK(c, c->bytes_b.ensure(n * 32));
-  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, c->ws.pts1.ensure(n));
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
-  launch_g1_mul(c->d_h, c->bytes_b.p, (int)n, c->pts1.p, c->stream);
-  launch_encode_g1(c->pts1.p, (int)n, c->bytes_a.p, c->stream);
+  launch_g1_mul(c->d_h, c->bytes_b.p, (int)n, c->ws.pts1.p, c->stream);
+  launch_encode_g1(c->ws.pts1.p, (int)n, c->bytes_a.p, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(sigs_out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
@@ -975,7 +1123,7 @@ void hg_destroy(hg_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->ws.side) (void)hipStreamSynchronize(c->ws.side);
   if (c->last_ev) (void)hipEventSynchronize(c->last_ev);  // a submission on a caller stream
   release_all(c);
   delete c;
@@ -1006,7 +1154,10 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   c->block_levels = 0;
   c->gt_level = 0;
   c->gt_requests = 0;
+  c->alt.gt_level = 0;  // both messages' tables are e(H, .) of the old registry
+  c->alt.gt_requests = 0;
   c->gt_cap = 2;
+  c->oom_cap = 2;
   // the previous registry's membership check must be done before its buffer is reused
   if (c->sub_pending) HG_CHECK(c, hipEventSynchronize(c->ev_sub));
   c->sub_pending = false;
@@ -1036,15 +1187,15 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   // decode above); the decode is complete (synchronised above)
   bool pending = false;
   if (c->flavor == HG_FLAVOR_GO && n) {
-    HG_CHECK(c, ensure_side(c));
+    HG_CHECK(c, ensure_side(c->ws));
     if (!c->ev_sub) HG_CHECK(c, hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
     HG_CHECK(c, c->sub_count.ensure(1));
-    HG_CHECK(c, hipMemsetAsync(c->sub_count.p, 0, sizeof(int), c->side));
-    launch_g2_subgroup(c->reg.p, (int)n, c->sub_count.p, c->side);
+    HG_CHECK(c, hipMemsetAsync(c->sub_count.p, 0, sizeof(int), c->ws.side));
+    launch_g2_subgroup(c->reg.p, (int)n, c->sub_count.p, c->ws.side);
     rc = check_launch(c);
     if (rc) return rc;
-    HG_CHECK(c, hipEventRecord(c->ev_sub, c->side));
-    (void)hipStreamQuery(c->side);  // flush: the check runs now, beside whatever follows
+    HG_CHECK(c, hipEventRecord(c->ev_sub, c->ws.side));
+    (void)hipStreamQuery(c->ws.side);  // flush: the check runs now, beside whatever follows
     pending = true;
   }
   // sums of the aligned power-of-two blocks (Handel's level ranges), level by level
@@ -1082,7 +1233,9 @@ int hg_registry_load(hg_ctx* c, const uint8_t* pks, size_t n, int32_t* codes) {
   return HG_OK;
 }
 
-static int prepare_aggregate_locked(hg_ctx* c) {
+// builds the tables up to `want` (-1: the highest the registry, the pin and
+// the device allow), synchronously
+static int prepare_aggregate_locked(hg_ctx* c, int want = -1) {
   if (!c->has_msg || c->nreg == 0) {
     c->err = "hg_prepare_aggregate: needs a message and a registry";
     return HG_ERR_ARG;
@@ -1092,20 +1245,14 @@ static int prepare_aggregate_locked(hg_ctx* c) {
   if (src) return src;
   int level = gt_max_level(c);
   if (c->pinned_level >= 0 && c->pinned_level < level) level = c->pinned_level;
+  if (want >= 0 && want < level) level = want;
   if (c->gt_level >= level) return HG_OK;
   HG_CHECK(c, hipSetDevice(c->device));
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
   // the highest level the device (and the table budget) can hold
-  while (level > c->gt_level) {
-    int rc = build_gt_locked(c, c->stream, level);
-    if (rc == kNoMem) {
-      gt_lower_cap(c, c->gt_level < level ? c->gt_level : level - 1);
-      level = level < c->gt_cap ? level : c->gt_cap;
-      continue;
-    }
-    if (rc) return rc;
-  }
+  int rc = build_fitting_locked(c, c->stream, level);
+  if (rc) return rc;
   HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
@@ -1143,11 +1290,13 @@ int hg_set_table_budget(hg_ctx* c, size_t bytes) {
   if (!c) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->table_budget = bytes;
-  // drop the built tables the new budget no longer covers; the cap is
-  // re-evaluated against the budget by the next build
+  // drop the built tables the new budget no longer covers (the cached
+  // message's first); the cap is re-evaluated against the budget by the next
+  // build, but never above what an out-of-memory failure left (oom_cap)
+  if (gt_table_bytes(c, c->gt_level) + alt_table_bytes(c) > bytes) drop_alt_tables(c);
   if (c->gt_level >= 1 && gt_table_bytes(c, c->gt_level) > bytes)
-    gt_lower_cap(c, gt_table_bytes(c, 1) <= bytes ? 1 : 0);
-  c->gt_cap = 2;
+    gt_lower_cap(c, gt_table_bytes(c, 1) <= bytes ? 1 : 0, false);
+  c->gt_cap = c->oom_cap;
   return HG_OK;
 }
 
@@ -1282,23 +1431,23 @@ int hg_combine_g1(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 64));
   HG_CHECK(c, c->bytes_b.ensure(n * 64));
-  HG_CHECK(c, c->pts1.ensure(n));
+  HG_CHECK(c, c->ws.pts1.ensure(n));
   HG_CHECK(c, c->pts1b.ensure(n));
   HG_CHECK(c, c->codes_a.ensure(n));
-  HG_CHECK(c, c->codes_b.ensure(n));
-  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, c->ws.codes_b.ensure(n));
+  HG_CHECK(c, c->ws.codes_c.ensure(n));
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, a, n * 64, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, b, n * 64, hipMemcpyHostToDevice, c->stream));
-  launch_decode_g1(c->bytes_a.p, (int)n, c->flavor, c->pts1.p, c->codes_a.p, c->stream);
-  launch_decode_g1(c->bytes_b.p, (int)n, c->flavor, c->pts1b.p, c->codes_b.p, c->stream);
-  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, c->codes_c.p, c->stream);
-  launch_g1_combine(c->pts1.p, c->pts1b.p, (int)n, c->bytes_a.p, c->stream);
+  launch_decode_g1(c->bytes_a.p, (int)n, c->flavor, c->ws.pts1.p, c->codes_a.p, c->stream);
+  launch_decode_g1(c->bytes_b.p, (int)n, c->flavor, c->pts1b.p, c->ws.codes_b.p, c->stream);
+  launch_merge_codes(c->codes_a.p, c->ws.codes_b.p, (int)n, c->ws.codes_c.p, c->stream);
+  launch_g1_combine(c->ws.pts1.p, c->pts1b.p, (int)n, c->bytes_a.p, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, c->bytes_a.p, n * 64, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->ws.codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
@@ -1310,24 +1459,24 @@ int hg_combine_g2(hg_ctx* c, const uint8_t* a, const uint8_t* b, size_t n, uint8
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 128 * 2));
-  HG_CHECK(c, c->pts2.ensure(n * 3));
+  HG_CHECK(c, c->ws.pts2.ensure(n * 3));
   HG_CHECK(c, c->codes_a.ensure(n));
-  HG_CHECK(c, c->codes_b.ensure(n));
-  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, c->ws.codes_b.ensure(n));
+  HG_CHECK(c, c->ws.codes_c.ensure(n));
   uint8_t* d = c->bytes_a.p;
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(d, a, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(d + n * 128, b, n * 128, hipMemcpyHostToDevice, c->stream));
-  launch_decode_g2(d, (int)n, c->flavor, c->pts2.p, c->codes_a.p, c->stream);
-  launch_decode_g2(d + n * 128, (int)n, c->flavor, c->pts2.p + n, c->codes_b.p, c->stream);
-  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, c->codes_c.p, c->stream);
-  launch_g2_combine(c->pts2.p, c->pts2.p + n, (int)n, c->pts2.p + 2 * n, c->stream);
-  launch_encode_g2(c->pts2.p + 2 * n, (int)n, d, c->stream);
+  launch_decode_g2(d, (int)n, c->flavor, c->ws.pts2.p, c->codes_a.p, c->stream);
+  launch_decode_g2(d + n * 128, (int)n, c->flavor, c->ws.pts2.p + n, c->ws.codes_b.p, c->stream);
+  launch_merge_codes(c->codes_a.p, c->ws.codes_b.p, (int)n, c->ws.codes_c.p, c->stream);
+  launch_g2_combine(c->ws.pts2.p, c->ws.pts2.p + n, (int)n, c->ws.pts2.p + 2 * n, c->stream);
+  launch_encode_g2(c->ws.pts2.p + 2 * n, (int)n, d, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(out, d, n * 128, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->ws.codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
@@ -1340,23 +1489,23 @@ int hg_pair(hg_ctx* c, const uint8_t* g1s, const uint8_t* g2s, size_t n, uint8_t
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 384));
   HG_CHECK(c, c->bytes_b.ensure(n * 64));
-  HG_CHECK(c, c->pts1.ensure(n));
-  HG_CHECK(c, c->pts2.ensure(n));
+  HG_CHECK(c, c->ws.pts1.ensure(n));
+  HG_CHECK(c, c->ws.pts2.ensure(n));
   HG_CHECK(c, c->codes_a.ensure(n));
-  HG_CHECK(c, c->codes_b.ensure(n));
-  HG_CHECK(c, c->codes_c.ensure(n));
+  HG_CHECK(c, c->ws.codes_b.ensure(n));
+  HG_CHECK(c, c->ws.codes_c.ensure(n));
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_a.p, g2s, n * 128, hipMemcpyHostToDevice, c->stream));
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, g1s, n * 64, hipMemcpyHostToDevice, c->stream));
-  launch_decode_g2(c->bytes_a.p, (int)n, HG_FLAVOR_GO, c->pts2.p, c->codes_a.p, c->stream);
-  launch_decode_g1(c->bytes_b.p, (int)n, HG_FLAVOR_GO, c->pts1.p, c->codes_b.p, c->stream);
-  launch_merge_codes(c->codes_a.p, c->codes_b.p, (int)n, c->codes_c.p, c->stream);
-  launch_pair(c->pts1.p, c->pts2.p, (int)n, c->d_lines, c->bytes_a.p, c->stream);
+  launch_decode_g2(c->bytes_a.p, (int)n, HG_FLAVOR_GO, c->ws.pts2.p, c->codes_a.p, c->stream);
+  launch_decode_g1(c->bytes_b.p, (int)n, HG_FLAVOR_GO, c->ws.pts1.p, c->ws.codes_b.p, c->stream);
+  launch_merge_codes(c->codes_a.p, c->ws.codes_b.p, (int)n, c->ws.codes_c.p, c->stream);
+  launch_pair(c->ws.pts1.p, c->ws.pts2.p, (int)n, c->d_lines, c->bytes_a.p, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(gt_out, c->bytes_a.p, n * 384, hipMemcpyDeviceToHost, c->stream));
-  HG_CHECK(c, hipMemcpyAsync(codes, c->codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HG_CHECK(c, hipMemcpyAsync(codes, c->ws.codes_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
   HG_CHECK(c, sub.finish());
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
@@ -1369,12 +1518,12 @@ int hg_keygen(hg_ctx* c, const uint8_t* scalars_be, size_t n, uint8_t* pks_out) 
   HG_CHECK(c, hipSetDevice(c->device));
   HG_CHECK(c, c->bytes_a.ensure(n * 128));
   HG_CHECK(c, c->bytes_b.ensure(n * 32));
-  HG_CHECK(c, c->pts2.ensure(n));
+  HG_CHECK(c, c->ws.pts2.ensure(n));
   Submission sub(c, c->stream);
   HG_CHECK(c, sub.start());
   HG_CHECK(c, hipMemcpyAsync(c->bytes_b.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
-  launch_g2_mul_base(c->bytes_b.p, (int)n, c->pts2.p, c->stream);
-  launch_encode_g2(c->pts2.p, (int)n, c->bytes_a.p, c->stream);
+  launch_g2_mul_base(c->bytes_b.p, (int)n, c->ws.pts2.p, c->stream);
+  launch_encode_g2(c->ws.pts2.p, (int)n, c->bytes_a.p, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HG_CHECK(c, hipMemcpyAsync(pks_out, c->bytes_a.p, n * 128, hipMemcpyDeviceToHost, c->stream));
@@ -1518,15 +1667,13 @@ int hg_packet_error(hg_ctx* c, int code, const hg_packet* p, char* buf, size_t c
 size_t hg_context_bytes(hg_ctx* c) {
   if (!c) return 0;
   std::lock_guard<std::mutex> g(c->mu);
-  size_t b = sizeof(LineCoef) * kNumLines + sizeof(PointG1) + 32;
+  size_t b = sizeof(LineCoef) * kNumLines + 2 * sizeof(PointG1) + 32;
   b += c->reg.cap * sizeof(PointG2) + c->blocks.cap * sizeof(PointG2) + c->wsum.cap * sizeof(PointG2);
-  b += c->bytes_a.cap + c->bytes_b.cap + c->pts2.cap * sizeof(PointG2) + c->pts1.cap * sizeof(PointG1);
-  b += c->pts1b.cap * sizeof(PointG1) + c->checks.cap * sizeof(CheckIn);
-  b += (c->codes_a.cap + c->codes_b.cap + c->codes_c.cap) * sizeof(int32_t) + c->reqs.cap * sizeof(hg_request);
-  b += c->order.cap * sizeof(int) + c->agg_ws.cap + c->words.cap * sizeof(uint64_t);
-  b += (c->gt_key.cap + c->gt_w8.cap + c->gt_win.cap + c->gt_blk.cap + c->gt_partial.cap + c->gt_y.cap) * sizeof(Gt);
-  b += c->gt_plan.cap * sizeof(GtReq) + c->gt_hdr.cap * sizeof(GtHdr) + c->gt_terms.cap * sizeof(uint32_t);
-  b += c->gt_ord.cap * sizeof(int2) + c->gt_multi.cap * sizeof(int) + c->gt_fe.cap * sizeof(Gt);
+  b += c->bytes_a.cap + c->bytes_b.cap + c->pts1b.cap * sizeof(PointG1);
+  b += c->codes_a.cap * sizeof(int32_t) + c->reqs.cap * sizeof(hg_request) + c->words.cap * sizeof(uint64_t);
+  b += (c->gt_key.cap + c->gt_w8.cap + c->gt_win.cap + c->gt_blk.cap) * sizeof(Gt) + alt_table_bytes(c);
+  b += c->ws.bytes();
+  for (const hg_lane* l : c->lanes) b += l->ws.bytes() + l->d_in.cap + l->d_codes.cap * sizeof(int32_t);
   b += c->sub_count.cap * sizeof(int) + c->pkts.cap * sizeof(hg_packet);
   return b;
 }
@@ -1588,5 +1735,132 @@ int hg_debug_fp_mul(hg_ctx* c, const uint32_t* a, const uint32_t* b, size_t n, u
   HG_CHECK(c, hipStreamSynchronize(c->stream));
   return HG_OK;
 }
+
+int hg_prepare_aggregate_level(hg_ctx* c, int level) {
+  if (!c || level < 0 || level > 2) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return prepare_aggregate_locked(c, level);
+}
+
+// ---------------------------------------------------------------- lanes
+int hg_lane_create(hg_ctx* c, size_t max_batch, size_t max_words, int overlap, hg_lane** out) {
+  if (!c || !out || max_batch == 0 || max_batch > (size_t)INT32_MAX || max_words > ((size_t)1 << 40))
+    return HG_ERR_ARG;
+  *out = nullptr;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  hg_lane* l = new hg_lane();
+  l->c = c;
+  l->overlap = overlap != 0;
+  l->max_batch = max_batch;
+  l->max_words = max_words;
+  // staging: requests | signatures | words, each 256-byte aligned
+  const size_t bytes = ((max_batch * sizeof(hg_request) + 255) & ~(size_t)255) +
+                       ((max_batch * 64 + 255) & ~(size_t)255) + max_words * 8 + 256;
+  hipError_t e = hipStreamCreateWithFlags(&l->s, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&l->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipHostMalloc(&l->h_in, bytes, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc(&l->h_codes, max_batch * sizeof(int32_t), hipHostMallocDefault);
+  if (e == hipSuccess) e = l->d_in.ensure(bytes);
+  if (e == hipSuccess) e = l->d_codes.ensure(max_batch);
+  if (e != hipSuccess) {
+    c->err = std::string("hg_lane_create: ") + hipGetErrorString(e);
+    l->ws.release();
+    l->d_in.release();
+    l->d_codes.release();
+    if (l->h_in) (void)hipHostFree(l->h_in);
+    if (l->h_codes) (void)hipHostFree(l->h_codes);
+    if (l->done) (void)hipEventDestroy(l->done);
+    if (l->s) (void)hipStreamDestroy(l->s);
+    delete l;
+    return HG_ERR_DEVICE;
+  }
+  c->lanes.push_back(l);
+  *out = l;
+  return HG_OK;
+}
+
+void hg_lane_destroy(hg_lane* l) {
+  if (!l) return;
+  hg_ctx* c = l->c;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(l->s);
+  if (l->ws.side) (void)hipStreamSynchronize(l->ws.side);
+  for (size_t i = 0; i < c->lanes.size(); i++)
+    if (c->lanes[i] == l) {
+      c->lanes.erase(c->lanes.begin() + (long)i);
+      break;
+    }
+  l->ws.release();
+  l->d_in.release();
+  l->d_codes.release();
+  (void)hipHostFree(l->h_in);
+  (void)hipHostFree(l->h_codes);
+  (void)hipEventDestroy(l->done);
+  (void)hipStreamDestroy(l->s);
+  delete l;
+}
+
+int hg_lane_stage(hg_lane* l, size_t n, size_t nwords, hg_request** reqs, uint8_t** sigs, uint64_t** words) {
+  if (!l || !reqs || !sigs || !words || n == 0 || n > l->max_batch || nwords > l->max_words) return HG_ERR_ARG;
+  l->n = n;
+  l->nwords = nwords;
+  l->off_sigs = (n * sizeof(hg_request) + 255) & ~(size_t)255;
+  l->off_words = (l->off_sigs + n * 64 + 255) & ~(size_t)255;
+  l->in_bytes = l->off_words + nwords * 8;
+  *reqs = reinterpret_cast<hg_request*>(l->h_in);
+  *sigs = l->h_in + l->off_sigs;
+  *words = reinterpret_cast<uint64_t*>(l->h_in + l->off_words);
+  return HG_OK;
+}
+
+int hg_lane_submit(hg_lane* l) {
+  if (!l || l->n == 0) return HG_ERR_ARG;
+  hg_ctx* c = l->c;
+  const size_t n = l->n;
+  const hg_request* h_reqs = reinterpret_cast<const hg_request*>(l->h_in);
+  // exact fold capacities from the requests (what aggregate_host_locked does),
+  // and no bitset read outside the staged words
+  FoldCaps caps;
+  for (size_t i = 0; i < n; i++) {
+    const hg_request& r = h_reqs[i];
+    if ((size_t)r.word_offset + ((size_t)r.bitlen + 63) / 64 > l->nwords) return HG_ERR_ARG;
+    caps.add(r.bitlen);
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  // after the context's last submission (a registry load, a hash, a table
+  // build); the lanes' own batches are independent of each other
+  if (c->last_ev) HG_CHECK(c, hipStreamWaitEvent(l->s, c->last_ev, 0));
+  uint8_t* d = l->d_in.p;
+  HG_CHECK(c, hipMemcpyAsync(d, l->h_in, l->in_bytes, hipMemcpyHostToDevice, l->s));
+  int rc = aggregate_device_locked(c, reinterpret_cast<const hg_request*>(d), n,
+                                   reinterpret_cast<const uint64_t*>(d + l->off_words), d + l->off_sigs,
+                                   l->d_codes.p, nullptr, nullptr, true, l->s, &caps, nullptr, l);
+  if (rc) return rc;
+  HG_CHECK(c, hipMemcpyAsync(l->h_codes, l->d_codes.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, l->s));
+  HG_CHECK(c, hipEventRecord(l->done, l->s));
+  l->recorded = true;
+  (void)hipStreamQuery(l->s);  // flush: start now
+  return HG_OK;
+}
+
+int hg_lane_query(hg_lane* l) {
+  if (!l) return -HG_ERR_ARG;
+  if (!l->recorded) return 1;
+  hipError_t e = hipEventQuery(l->done);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  return -HG_ERR_DEVICE;
+}
+
+int hg_lane_wait(hg_lane* l) {
+  if (!l) return HG_ERR_ARG;
+  if (!l->recorded) return HG_OK;
+  return hipEventSynchronize(l->done) == hipSuccess ? HG_OK : HG_ERR_DEVICE;
+}
+
+const int32_t* hg_lane_codes(hg_lane* l) { return l ? l->h_codes : nullptr; }
 
 }  // extern "C"

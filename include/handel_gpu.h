@@ -346,6 +346,79 @@ int hg_batcher_verify_aggregate(hg_batcher* b, const uint8_t* msg, size_t len, c
                                 const uint64_t* words, const uint8_t* sig, int32_t* code);
 int hg_batcher_stats(hg_batcher* b, uint64_t* batches, uint64_t* requests);
 
+/* ---------------------------------------------------------------- lanes
+ * Several aggregate batches of one context in flight at once. A lane owns a
+ * stream, device workspaces and pinned host staging; lanes share the
+ * context's registry, hashed message and GT tables, which are read-only while
+ * lanes run. A lane batch verifies against the context's CURRENT message
+ * (hg_set_message / hg_prepare_aggregate_msg, called with every lane idle)
+ * at the table level already built (hg_prepare_aggregate*): a lane never
+ * builds tables. Used by the verifier service below; one thread per lane.
+ * Lanes must be destroyed before their context. */
+typedef struct hg_lane hg_lane;
+/* max_batch requests and max_words bitset words per batch; overlap: the GT
+ * fold beside the pairing kernel on a second stream of the lane. */
+int hg_lane_create(hg_ctx* ctx, size_t max_batch, size_t max_words, int overlap, hg_lane** out);
+void hg_lane_destroy(hg_lane* lane);
+/* Pinned staging of the next batch: n requests (word_offset relative to
+ * *words), their 64-byte signatures, nwords bitset words. The lane must be
+ * idle. The pointers stay valid until the next hg_lane_stage. */
+int hg_lane_stage(hg_lane* lane, size_t n, size_t nwords, hg_request** reqs, uint8_t** sigs, uint64_t** words);
+/* Enqueues the staged batch (one host-to-device copy, the GT or G2 path,
+ * the codes back to pinned memory); asynchronous. */
+int hg_lane_submit(hg_lane* lane);
+/* 1: the last batch is done (hg_lane_codes valid), 0: running, else an error code. */
+int hg_lane_query(hg_lane* lane);
+int hg_lane_wait(hg_lane* lane);
+/* The last batch's n codes (pinned host memory, valid once it is done). */
+const int32_t* hg_lane_codes(hg_lane* lane);
+/* Builds the GT tables of the current message up to `level` (0..2, capped as
+ * hg_prepare_aggregate caps) now; for owners of lanes that follow the volume
+ * policy themselves. Synchronous. */
+int hg_prepare_aggregate_level(hg_ctx* ctx, int level);
+
+/* ---------------------------------------------------------------- verifier service
+ * ONE process owns the GPU, the context, the registry and ONE set of GT
+ * tables, and verifies the aggregate checks of many client processes that
+ * reach it through a POSIX shared-memory object `name` (shm_open). Clients
+ * use include/handel_client.h (libhandel_client.so: no GPU, no HIP runtime),
+ * so simul's single-host layout — P OS processes of k Handel instances each
+ * (simul/node/main.go:63-131), every instance's evaluator checking one
+ * multisignature at a time (processing.go:228-287 -> verifySignature
+ * :342-368) — shares one GPU without a HIP context per process. A dispatcher
+ * thread merges queued requests into batches (grouped by message, at most
+ * max_batch) and keeps up to `lanes` batches in flight (hg_lane_*); each
+ * client learns its own verdicts. The context must outlive the service and
+ * must not be used by others while it runs (the service switches its message
+ * and builds its tables). */
+typedef struct hg_service hg_service;
+typedef struct {
+  uint32_t slots;       /* request slots in the region (multiple of 64; default 8192) */
+  uint32_t slot_bits;   /* largest bitset of one request (default: the registry size) */
+  uint32_t channels;    /* client handles attached at once (default 256) */
+  uint32_t lanes;       /* batches in flight on the GPU (default 8) */
+  uint32_t max_batch;   /* requests per batch (default 4096) */
+  uint32_t max_wait_us; /* a queued request waits at most this long for more to batch with (default 50) */
+  int32_t prepare;      /* 1 (default): a message's first batch builds its top GT table level;
+                           0: the context's volume policy (levels 1 and 2 after 16384 / 2^20 requests) */
+  int32_t overlap;      /* 1 (default): the GT fold beside the pairing kernel inside each lane */
+} hg_service_config;
+void hg_service_config_init(hg_service_config* cfg);
+/* Creates the region (fails if `name` exists) and starts the dispatcher. */
+int hg_service_create(hg_ctx* ctx, const char* name, const hg_service_config* cfg, hg_service** out);
+/* The same protocol served by a CPU stand-in for the GPU (protocol tests
+ * without a GPU): a request's code is HG_ERR_LEVEL if it fails the level
+ * check against an nreg-key registry, 77 if its bitset words do not match
+ * sig[1..8] (the xor of the words, little-endian), else HG_ERR_SIG_INVALID
+ * if sig[0] == 1, else HG_OK; each batch completes delay_us after launch. */
+int hg_service_create_echo(const char* name, const hg_service_config* cfg, uint32_t nreg, uint32_t delay_us,
+                           hg_service** out);
+/* Verifies what is queued, stops the dispatcher, wakes every client and
+ * removes the region's name. */
+void hg_service_destroy(hg_service* svc);
+/* batches launched, requests verified, most batches in flight at once */
+int hg_service_stats(hg_service* svc, uint64_t* batches, uint64_t* requests, uint64_t* max_in_flight);
+
 #ifdef __cplusplus
 }
 #endif

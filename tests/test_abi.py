@@ -12,10 +12,10 @@ from handel_amd import build as B
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    text = open(os.path.join(ROOT, "include", "handel_gpu.h")).read()
+def declared_symbols(header="handel_gpu.h"):
+    text = open(os.path.join(ROOT, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"^\s*(?:int|void|size_t|const char\*)\s+(hg_\w+)\s*\(", text, flags=re.M))
+    return set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_]\w*\s*\**\s*(hg_\w+)\s*\(", text, flags=re.M))
 
 
 def test_header_declares_expected_entry_points():
