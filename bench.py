@@ -253,6 +253,27 @@ def pmc_traffic(pattern: str):
     return sum(got.values()), ", ".join(sorted(srcs))
 
 
+def rocprof_kernel_us(pattern: str):
+    """Average duration (us) of the kernels matching `pattern` in the newest
+    committed kernel-trace summary of the DRIVER's invocation
+    (profiles/*_driver_ktrace_stats.csv: rocprofv3 --kernel-trace --stats of
+    `bench.py --steps 20 --warmup 5`, tools/gpu_pin.sh), summed over the
+    matching kernels; (None, None) if no summary holds them."""
+    import csv
+    import glob
+    import re
+
+    def key(path):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_driver_ktrace_stats.csv")), key=key, reverse=True):
+        with open(path) as f:
+            rows = [r for r in csv.DictReader(f) if re.search(pattern, r["kernel"])]
+        if rows:
+            return sum(float(r["avg_us"]) for r in rows), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def _cgroup_quota_cpus():
     """CPUs of CPU time the cgroup grants this process (cgroup v2 cpu.max
     "quota period"), None when unlimited or unreadable."""
@@ -373,10 +394,25 @@ def cpu_baseline_aggregate(reg: bytes, reqs, words, sigs: bytes, expect: np.ndar
 
 
 class Timer:
-    """Barrier + synchronize on both sides of the timed region, max over ranks."""
+    """Barrier + synchronize on both sides of the timed region, max over ranks
+    (every rank's own time is kept in `rank_times`)."""
 
-    def __init__(self, dev, dist, coll_dev):
-        self.dev, self.dist, self.coll_dev = dev, dist, coll_dev
+    def __init__(self, dev, dist, coll_dev, world: int = 1):
+        self.dev, self.dist, self.coll_dev, self.world = dev, dist, coll_dev, world
+        self.rank_times = []
+
+    def prewarm(self, step, seconds: float) -> int:
+        """Untimed steps for `seconds` of wall time before the warmup steps, so
+        the GPU's clocks have settled whatever the warmup count; returns the
+        steps run (reported in the line)."""
+        k, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            step()
+            k += 1
+            if k % 16 == 0:
+                torch.cuda.synchronize(self.dev)
+        torch.cuda.synchronize(self.dev)
+        return k
 
     def run(self, step, steps: int, warmup: int) -> float:
         for _ in range(warmup):
@@ -393,10 +429,13 @@ class Timer:
         if self.dist:
             tdist.barrier()
         dt = time.perf_counter() - t0
+        self.rank_times = [dt]
         if self.dist:
             t = torch.tensor([dt], dtype=torch.float64, device=self.coll_dev)
-            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-            dt = float(t.item())
+            every = [torch.zeros_like(t) for _ in range(self.world)]
+            tdist.all_gather(every, t)
+            self.rank_times = [float(x.item()) for x in every]
+            dt = max(self.rank_times)
         return dt
 
 
@@ -569,6 +608,39 @@ def packet_intake(eng: Engine, head, n_reg: int, dev, stream, timer, args, world
                          "note": "a 4096-packet launch is launch/latency bound; the fraction says so"}}
 
 
+def batch_latency(eng: Engine, head, dev, sizes=(32, 128, 512, 4096), reps: int = 15):
+    """The small-batch floor: wall time of ONE batch of n requests, submitted
+    alone and waited for (the first n requests of the headline batch). 'device':
+    inputs resident in HBM (hg_verify_aggregate_device + synchronize); 'host':
+    host buffers in and codes out (hg_verify_aggregate: what a batcher or the
+    verifier service pays per batch). Median over reps. A batch of n <= 4096
+    checks holds one pairing wave per SIMD at most, so its latency is one
+    pairing kernel whatever n is."""
+    out = {}
+    s = torch.cuda.Stream(dev)
+    for m in sizes:
+        m = min(m, head.n)
+        codes = torch.zeros(m, dtype=torch.int32, device=dev)
+        dev_t, host_t = [], []
+        r = head.reqs[:m]
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            eng.verify_aggregate_device(head.d_reqs.data_ptr(), m, head.d_words.data_ptr(), head.d_sigs.data_ptr(),
+                                        codes.data_ptr(), 0, s.cuda_stream)
+            s.synchronize()
+            dev_t.append(time.perf_counter() - t0)
+        assert np.array_equal(codes.cpu().numpy(), head.expect[:m])
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            got = eng.verify_aggregate(r, head.words, head.sigs[:64 * m])
+            host_t.append(time.perf_counter() - t0)
+        assert np.array_equal(got, head.expect[:m])
+        d, h = float(np.median(dev_t)) * 1e3, float(np.median(host_t)) * 1e3
+        out[str(m)] = {"device_ms": round(d, 4), "host_ms": round(h, 4),
+                       "verif_per_s_device": round(m / d * 1e3, 1), "verif_per_s_host": round(m / h * 1e3, 1)}
+    return out
+
+
 def timed_phases(eng: Engine, run):
     """Runs run() with the engine's HIP-event timing on; returns per-phase
     (mean ms per interval) for verify / aggregate fold / whole submission."""
@@ -585,12 +657,22 @@ def timed_phases(eng: Engine, run):
     return out
 
 
-def roofline(fpmul: int, ms: float, kernel: str, traffic_pattern: str, work: str):
+def roofline(fpmul: int, ms: float, kernel: str, traffic_pattern: str, work: str, rocprof_pattern: str = None):
+    """VALU roofline of `fpmul` Fp multiplications over `ms` (HIP events on the
+    launch stream). rocprof_pattern: the kernels whose summed rocprof average
+    (the driver-invocation profile) gives the same work's `frac_rocprof`."""
     achieved = fpmul * MADS_PER_FPMUL / (ms * 1e-3) / 1e12
     traffic, src = pmc_traffic(traffic_pattern)
-    return {"bound": "valu", "achieved": round(achieved, 3), "peak": P_MAD_TOPS, "unit": "Tmad/s",
-            "frac": round(achieved / P_MAD_TOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-            "traffic_source": src, "kernel": kernel, "kernel_ms": round(ms, 4), "work": work}
+    out = {"bound": "valu", "achieved": round(achieved, 3), "peak": P_MAD_TOPS, "unit": "Tmad/s",
+           "frac": round(achieved / P_MAD_TOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+           "traffic_source": src, "kernel": kernel, "kernel_ms": round(ms, 4), "work": work}
+    if rocprof_pattern:
+        us, rsrc = rocprof_kernel_us(rocprof_pattern)
+        if us:
+            out["rocprof_kernel_ms"] = round(us / 1e3, 4)
+            out["frac_rocprof"] = round(fpmul * MADS_PER_FPMUL / (us * 1e-6) / 1e12 / P_MAD_TOPS, 4)
+            out["rocprof_source"] = rsrc
+    return out
 
 
 def main():
@@ -607,6 +689,8 @@ def main():
     ap.add_argument("--pipeline-overlap", type=int, default=1,
                     help="the pipelined line's contexts run their fold beside the pairing kernel (1) or before it (0)")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="requests in the CPU baseline's sample")
+    ap.add_argument("--prewarm", type=float, default=0.3,
+                    help="seconds of untimed headline steps before the warmup steps (GPU clocks settle)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -631,7 +715,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local_dev)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
-    timer = Timer(dev, dist, coll_dev)
+    timer = Timer(dev, dist, coll_dev, world)
     stream = torch.cuda.current_stream(dev)
     n = args.batch
 
@@ -647,16 +731,22 @@ def main():
         head.submit_bits()
         gather_verdicts(head.d_bits.to(coll_dev), world, gathered)
 
-    for _ in range(max(args.warmup, 1)):
-        step()
+    step()
     torch.cuda.synchronize(dev)
     head.check()
     assert torch.equal(head.d_bits, pack_verdicts(head.d_codes)), "HIP verdict bitset differs from the codes"
+    prewarm_steps = timer.prewarm(step, args.prewarm)
     dt = timer.run(step, args.steps, args.warmup)
+    rank_ms = [round(t / args.steps * 1e3, 4) for t in timer.rank_times]
     head.check()
-    if dist:
-        want = [pack_verdicts(torch.from_numpy(head.expect))]
-        assert torch.equal(gathered[rank].cpu(), want[0]), "gathered bitset of this rank differs"
+    # every rank's gathered bitset: each rank tampers every 8th aggregate of
+    # its own batch, so all world bitsets equal this rank's expected one
+    want = pack_verdicts(torch.from_numpy(head.expect))
+    gather_check = {"world_size_seen": tdist.get_world_size() if dist else 1, "backend": backend if dist else None,
+                    "ranks_checked": world}
+    for r in range(world):
+        g = gathered[r] if dist else head.d_bits
+        assert torch.equal(g.cpu(), want), f"gathered bitset of rank {r} differs"
     ph = timed_phases(eng, lambda: [head.submit() for _ in range(5)])
     # the kernels on their own (fold, then the pairing kernel: no overlap),
     # for the per-kernel rooflines
@@ -671,11 +761,15 @@ def main():
     agg_ms = ph["submit"]
     impl_fpmul = head.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING
     roof = roofline(impl_fpmul, agg_ms, "the GT submission: k_agg_prologue, k_verify_sig beside the GT fold "
-                    "(k_gt_plan, k_gt_chunks, k_gt_combine), k_gt_compare",
-                    r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare)|k_verify_sig<4, true>",
+                    "(k_gt_plan, k_gt_chunks, k_gt_combine), k_gt_compare_bits",
+                    r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare_bits)|k_verify_sig<4, true>",
                     f"implemented work: {head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 "
                     f"product each) + {n} x {FPMUL_PER_SIG_PAIRING} Fp-mul (one pairing + final exponentiation "
-                    f"per check), x {MADS_PER_FPMUL} u32 mads")
+                    f"per check), x {MADS_PER_FPMUL} u32 mads",
+                    rocprof_pattern=r"k_verify_sig<4, true>|k_gt_compare_bits")
+    roof["frac_rocprof_note"] = ("the same work over the rocprof averages of the step's critical path (the pairing "
+                                 "kernel, then the comparison; the fold runs beside it) in the driver-invocation "
+                                 "profile")
     roof["kernels_ms"] = {"fold": round(ph["fold"], 4), "k_verify": round(ph["verify"], 4),
                           "submit": round(ph["submit"], 4)}
     # the reference algorithm's work over the same time: a rate, not a
@@ -688,7 +782,8 @@ def main():
                  "note": "work the GT path does not run is credited here; not a fraction of any peak"}
     roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph_seq["verify"], "k_verify_sig", r"k_verify_sig<4, false>",
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
-                           "+ final exponentiation, oracle op count); kernel alone (fold not beside it)")
+                           "+ final exponentiation, oracle op count); kernel alone (fold not beside it)",
+                           rocprof_pattern=r"k_verify_sig<4, true>")
     roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph_seq["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
                          r"k_gt_(plan<16>|chunks|combine)",
                          f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each); "
@@ -763,7 +858,7 @@ def main():
             "kernels_ms": {k: round(v, 4) for k, v in fph.items() if v is not None},
             "roofline": roofline(full.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING, fph["submit"],
                                  "the GT submission (as the headline)",
-                                 r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare)|k_verify_sig<4, true>",
+                                 r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare(?!_))|k_verify_sig<4, true>",
                                  f"implemented work: {full.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul + "
                                  f"{n} x {FPMUL_PER_SIG_PAIRING} Fp-mul, x {MADS_PER_FPMUL} u32 mads")}
         del full
@@ -799,6 +894,10 @@ def main():
             eng.set_fold_overlap(True)
 
         extra["packet_intake"] = packet_intake(eng, head, n_reg, dev, stream, timer, args, world)
+        extra["batch_latency"] = {
+            "what": "one batch submitted alone and waited for (median of 15), first n headline requests: the "
+                    "per-check latency floor a one-check-at-a-time evaluator (processing.go:228-287) sees",
+            **batch_latency(eng, head, dev)}
         extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)
 
     cpu = None
@@ -819,6 +918,11 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
+            "prewarm": {"seconds": args.prewarm, "steps": prewarm_steps, "what": "untimed headline steps before the "
+                        "warmup steps (GPU clocks settled whatever the warmup count)"},
+            "gather": {**gather_check, "what": "every rank's all-gathered verdict bitset checked against the expected "
+                       "one (world 1: the gather is the identity, the rank's own bitset is checked)"},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -26,15 +26,20 @@
 
 #include "../../include/handel_gpu.h"
 
+// A ticket carries its own completion state: hg_batcher_wait touches only
+// the ticket, so a wait may outlive the batcher (hg_batcher_destroy verifies
+// every queued ticket before it returns).
 struct hg_ticket {
   std::string msg;
   hg_request req{};
   std::vector<uint64_t> words;
   uint8_t sig[64];
-  int32_t code = HG_OK;
+  std::chrono::steady_clock::time_point t_submit;
+  std::mutex mu;
+  std::condition_variable cv;
+  int32_t code = HG_OK;  // guarded by mu
   int rc = HG_OK;
   bool done = false;
-  std::chrono::steady_clock::time_point t_submit;
 };
 
 struct hg_batcher {
@@ -43,7 +48,6 @@ struct hg_batcher {
   std::chrono::microseconds max_wait{200};
   std::mutex mu;
   std::condition_variable cv_queue;  // the dispatcher waits for requests
-  std::condition_variable cv_done;   // callers wait for their request's batch
   std::deque<hg_ticket*> queue;
   bool stop = false;
   uint64_t batches = 0, requests = 0;
@@ -93,15 +97,19 @@ void hg_batcher::run() {
     const int rc = hg_verify_aggregate_msg(ctx, reinterpret_cast<const uint8_t*>(msg.data()), msg.size(),
                                            reqs.data(), n, words.empty() ? nullptr : words.data(), words.size(),
                                            sigs.data(), codes.data(), nullptr);
-    lk.lock();
+    // notify under each ticket's lock: once it is released the waiter may
+    // delete the ticket, so nothing touches it afterwards
     for (size_t i = 0; i < n; i++) {
-      take[i]->rc = rc;
-      take[i]->code = rc == HG_OK ? codes[i] : rc;
-      take[i]->done = true;
+      hg_ticket* t = take[i];
+      std::lock_guard<std::mutex> g(t->mu);
+      t->rc = rc;
+      t->code = rc == HG_OK ? codes[i] : rc;
+      t->done = true;
+      t->cv.notify_one();
     }
+    lk.lock();
     batches++;
     requests += n;
-    cv_done.notify_all();
   }
 }
 
@@ -126,7 +134,7 @@ void hg_batcher_destroy(hg_batcher* b) {
   }
   b->cv_queue.notify_all();
   b->th.join();  // queued requests are verified first; their callers still own the tickets
-  delete b;
+  delete b;       // tickets never point back at the batcher
 }
 
 int hg_batcher_submit(hg_batcher* b, const uint8_t* msg, size_t len, const hg_request* req, const uint64_t* words,
@@ -154,12 +162,15 @@ int hg_batcher_submit(hg_batcher* b, const uint8_t* msg, size_t len, const hg_re
 }
 
 int hg_batcher_wait(hg_batcher* b, hg_ticket* t, int32_t* code) {
-  if (!b || !t) return HG_ERR_ARG;
-  std::unique_lock<std::mutex> lk(b->mu);
-  b->cv_done.wait(lk, [&] { return t->done; });
-  lk.unlock();
-  const int rc = t->rc;
-  if (code) *code = t->code;
+  (void)b;  // the ticket holds everything (it may outlive the batcher)
+  if (!t) return HG_ERR_ARG;
+  int rc;
+  {
+    std::unique_lock<std::mutex> lk(t->mu);
+    t->cv.wait(lk, [&] { return t->done; });
+    rc = t->rc;
+    if (code) *code = t->code;
+  }
   delete t;
   return rc;
 }

@@ -38,7 +38,10 @@ def unpack_verdicts(bits: torch.Tensor, n: int) -> torch.Tensor:
 
 
 def gather_verdicts(bits: torch.Tensor, world: int, out: List[torch.Tensor] = None) -> List[torch.Tensor]:
-    """all_gather of equal-size bitsets (every rank gets every rank's verdicts)."""
+    """all_gather of equal-size bitsets (every rank gets every rank's verdicts).
+    With one rank the gather is the identity and copies nothing: the result
+    (and out[0], when `out` is given) IS `bits`, so it changes when the caller
+    rewrites `bits` (bench.py's world-1 step gathers nothing, and says so)."""
     import torch.distributed as dist
 
     if world == 1:  # one rank: the gather is the identity

@@ -380,6 +380,8 @@ class Batcher:
         m = _u8(msg)
         req = np.array([(offset, bitlen, level_size, 0)], dtype=REQ_DTYPE)
         w = np.ascontiguousarray(words, dtype=np.uint64)
+        if len(w) < (int(bitlen) + 63) // 64:  # hg_batcher_submit copies ceil(bitlen / 64) words
+            raise ValueError(f"{bitlen} bits need {(int(bitlen) + 63) // 64} words, got {len(w)}")
         sg = _u8(sig)
         if len(sg) != 64:
             raise ValueError("signature must be 64 bytes")

@@ -16,9 +16,21 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import partitioner as part
-from ._lib import HG_OK
+from ._lib import HG_ERR_SIG_CF_SHORT, HG_ERR_SIG_UNMARSHAL, HG_OK
 from .engine import REQ_DTYPE, Engine
 from .sigprocessing import IncomingSig, MultiSig, int_to_words
+
+
+def sig_length_code(flavor: str, sig: bytes) -> int:
+    """SigBLS.UnmarshalBinary's length rule: x/crypto's G1.Unmarshal wants
+    exactly 64 bytes (bn256/go/bn256.go:182-190 -> "bn256: multisig can't
+    unmarshal"); cloudflare's wants at least 64 and ignores the rest
+    (bn256/cf/bn256.go:183-190 -> "...: bn256: not enough data"). HG_OK when
+    the length passes (the point itself is checked on the GPU)."""
+    n = len(sig)
+    if flavor in ("cf", "bn256/cf", "bn256"):
+        return HG_ERR_SIG_CF_SHORT if n < 64 else HG_OK
+    return HG_ERR_SIG_UNMARSHAL if n != 64 else HG_OK
 
 
 class BatchVerifier:
@@ -36,22 +48,35 @@ class BatchVerifier:
         self.node_id = node_id
 
     def _pack(self, items):
-        reqs = np.zeros(len(items), dtype=REQ_DTYPE)
+        """items whose signature passes the length rule go into one batch
+        (cloudflare's extra bytes dropped, as its Unmarshal does); the others
+        keep their unmarshal code and are never submitted"""
+        pre = np.array([sig_length_code(self.eng.flavor_name, bytes(it[3])) for it in items], dtype=np.int32)
+        keep = [i for i in range(len(items)) if pre[i] == HG_OK]
+        reqs = np.zeros(len(keep), dtype=REQ_DTYPE)
         words: List[np.ndarray] = []
         nw = 0
         sigs = bytearray()
-        for i, (lo, size, bits, sig) in enumerate(items):
+        for j, i in enumerate(keep):
+            lo, size, bits, sig = items[i]
             if isinstance(bits, MultiSig):
                 w, bitlen = int_to_words(bits.bits, bits.bitlen), bits.bitlen
             else:
                 w, bitlen = part.bits_to_words(bits), len(bits)
-            reqs[i] = (lo, bitlen, size, nw)
+            reqs[j] = (lo, bitlen, size, nw)
             words.append(w)
             nw += len(w)
-            s = bytes(sig)
-            sigs += s[:64].ljust(64, b"\x00") if len(s) != 64 else s
+            sigs += bytes(sig)[:64]
         allw = np.concatenate(words) if words else np.zeros(0, dtype=np.uint64)
-        return reqs, allw, bytes(sigs)
+        return (reqs, allw, bytes(sigs)), pre, keep
+
+    def _codes(self, items) -> np.ndarray:
+        """codes of (offset, level_size, bits, sig) items: the length rule's
+        unmarshal codes, the GPU's for the rest"""
+        batch, codes, keep = self._pack(items)
+        if keep:
+            codes[np.array(keep)] = self.eng.verify_aggregate(*batch)
+        return codes
 
     def verify_levels(self, sigs: Sequence[IncomingSig]) -> List[Optional[str]]:
         """verifySignature (processing.go:342-368) for each incoming sig, as
@@ -71,13 +96,16 @@ class BatchVerifier:
             except part.PartitionerError as e:
                 items.append((0, 0, [], bytes(64)))
                 errs.append(str(e))
-        codes = self.eng.verify_aggregate(*self._pack(items)) if items else []
+        codes = self._codes(items) if items else []
         out = []
         for e, c in zip(errs, codes):
             if e is not None:
                 out.append(e)
             elif c == HG_OK:
                 out.append(None)
+            elif c in (HG_ERR_SIG_UNMARSHAL, HG_ERR_SIG_CF_SHORT):
+                # the signature never parses (MultiSignature.Unmarshal, crypto.go:86-110)
+                out.append(self.eng.code_string(int(c)))
             else:
                 # processing.go:350-352 returns the level error as is; only
                 # VerifySignature's errors are wrapped "handel: ..." (:361-365)
@@ -122,7 +150,7 @@ class BatchVerifier:
 
     def verify_ranges(self, items) -> np.ndarray:
         """Raw codes for (offset, level_size, bits, sig) requests."""
-        return self.eng.verify_aggregate(*self._pack(items))
+        return self._codes(items)
 
     def verify_multisignature(self, bits: Sequence[bool], sig: bytes) -> Optional[str]:
         """crypto.go:120-137 VerifyMultiSignature over the whole registry
@@ -131,16 +159,19 @@ class BatchVerifier:
 
     def verify_multisignatures(self, items) -> List[Optional[str]]:
         """VerifyMultiSignature for each (bits, sig) in one GPU batch."""
+        codes = np.array([sig_length_code(self.eng.flavor_name, bytes(sig)) for _, sig in items], dtype=np.int32)
+        keep = [i for i in range(len(items)) if codes[i] == HG_OK]
         words, bitlens, woffs, sigs = [], [], [], bytearray()
         nw = 0
-        for bits, sig in items:
+        for i in keep:
+            bits, sig = items[i]
             w = part.bits_to_words(bits)
             words.append(w)
             bitlens.append(len(bits))
             woffs.append(nw)
             nw += len(w)
-            s = bytes(sig)
-            sigs += s[:64].ljust(64, b"\x00") if len(s) != 64 else s
+            sigs += bytes(sig)[:64]
         allw = np.concatenate(words) if words else np.zeros(0, dtype=np.uint64)
-        codes = self.eng.verify_multisig(bitlens, woffs, allw, bytes(sigs))
+        if keep:
+            codes[np.array(keep)] = self.eng.verify_multisig(bitlens, woffs, allw, bytes(sigs))
         return [None if c == HG_OK else self.eng.code_string(int(c)) for c in codes]

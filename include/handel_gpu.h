@@ -330,7 +330,9 @@ int hg_packet_error(hg_ctx* ctx, int code, const hg_packet* p, char* buf, size_t
 typedef struct hg_batcher hg_batcher;
 typedef struct hg_ticket hg_ticket;
 int hg_batcher_create(hg_ctx* ctx, size_t max_batch, unsigned max_wait_us, hg_batcher** out);
-/* Verifies what is still queued, then stops the dispatcher. */
+/* Verifies what is still queued, then stops the dispatcher. Tickets stay
+ * valid: hg_batcher_wait on a ticket submitted before the destroy returns its
+ * code even after the batcher is gone (a ticket holds its own state). */
 void hg_batcher_destroy(hg_batcher* b);
 /* Queues one request: req->offset / bitlen / level_size as in hg_request
  * (word_offset ignored), its ceil(bitlen/64) bitset words at `words`, the

@@ -171,7 +171,8 @@ def test_gpu_multisig_golden(engine, gv, registry):
     for q in ms["requests"]:
         bits = O.bitset_unmarshal(b(q["bitset"]))
         items.append((q["lo"], q["hi"] - q["lo"], bits, b(q["agg_sig"])))
-    reqs, words, sigs = bv._pack(items)
+    (reqs, words, sigs), pre, _ = bv._pack(items)
+    assert not pre.any()  # every golden signature is 64 bytes
     codes, agg = engine.verify_aggregate(reqs, words, sigs, want_agg=True)
     assert list(codes) == [q["code"] for q in ms["requests"]]
     for i, q in enumerate(ms["requests"]):
