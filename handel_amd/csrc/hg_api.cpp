@@ -1763,6 +1763,28 @@ int hg_lane_create(hg_ctx* c, size_t max_batch, size_t max_words, int overlap, h
   if (e == hipSuccess) e = hipHostMalloc(&l->h_codes, max_batch * sizeof(int32_t), hipHostMallocDefault);
   if (e == hipSuccess) e = l->d_in.ensure(bytes);
   if (e == hipSuccess) e = l->d_codes.ensure(max_batch);
+  // every workspace at its largest now (max_batch requests over max_words
+  // bitset words): a buffer that grew later would be freed and reallocated
+  // between batches, and hipFree waits for the whole device
+  const size_t n = max_batch;
+  const size_t terms = 8 * (max_words + n) + n;  // sum of fold_terms_bound over the batch
+  const size_t chunks = terms / (size_t)gt_chunk() + n;
+  Ws& w = l->ws;
+  if (e == hipSuccess) e = w.pts1.ensure(n);
+  if (e == hipSuccess) e = w.codes_b.ensure(n);
+  if (e == hipSuccess) e = w.codes_c.ensure(n);
+  if (e == hipSuccess) e = w.checks.ensure(n);
+  if (e == hipSuccess) e = w.order.ensure(n);
+  if (e == hipSuccess) e = w.agg_ws.ensure(n * agg_partial_bytes() + agg_fixed_bytes());
+  if (e == hipSuccess) e = w.gt_plan.ensure(n);
+  if (e == hipSuccess) e = w.gt_hdr.ensure(1);
+  if (e == hipSuccess) e = w.gt_terms.ensure(terms);
+  if (e == hipSuccess) e = w.gt_ord.ensure(chunks);
+  if (e == hipSuccess) e = w.gt_multi.ensure(2 * n);
+  if (e == hipSuccess) e = w.gt_partial.ensure(chunks);
+  if (e == hipSuccess) e = w.gt_y.ensure(n);
+  if (e == hipSuccess) e = w.gt_fe.ensure(n);
+  if (e == hipSuccess && l->overlap) e = ensure_side(w);
   if (e != hipSuccess) {
     c->err = std::string("hg_lane_create: ") + hipGetErrorString(e);
     l->ws.release();

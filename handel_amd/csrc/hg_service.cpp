@@ -56,7 +56,23 @@ struct Exec {
 struct GpuExec : Exec {
   hg_ctx* ctx;
   std::vector<hg_lane*> ln;
+  bool warmed = false;
   explicit GpuExec(hg_ctx* c) : ctx(c) {}
+  // one tiny batch per lane, waited for: every kernel of the path is loaded
+  // and every lane's stream has run once before the first client's batch
+  void warm_up() {
+    for (hg_lane* l : ln) {
+      hg_request* r = nullptr;
+      uint8_t* s = nullptr;
+      uint64_t* w = nullptr;
+      if (hg_lane_stage(l, 1, 1, &r, &s, &w) != HG_OK) continue;
+      r[0] = hg_request{0, 1, 1, 0};
+      w[0] = 1;
+      memset(s, 0, 64);
+      if (hg_lane_submit(l) == HG_OK) (void)hg_lane_wait(l);
+    }
+    warmed = true;
+  }
   ~GpuExec() override {
     for (hg_lane* l : ln) hg_lane_destroy(l);
   }
@@ -68,7 +84,9 @@ struct GpuExec : Exec {
   int query(int i) override { return hg_lane_query(ln[i]); }
   const int32_t* codes(int i) override { return hg_lane_codes(ln[i]); }
   int use_message(const uint8_t* m, size_t len, bool prepare) override {
-    return prepare ? hg_prepare_aggregate_msg(ctx, m, len) : hg_set_message(ctx, m, len);
+    const int rc = prepare ? hg_prepare_aggregate_msg(ctx, m, len) : hg_set_message(ctx, m, len);
+    if (rc == HG_OK && !warmed) warm_up();
+    return rc;
   }
   int build_level(int level) override { return hg_prepare_aggregate_level(ctx, level); }
 };

@@ -117,6 +117,10 @@ class Engine:
         """Registry keys on the twist but outside G2 (hg_registry_non_g2)."""
         return int(self.L.hg_registry_non_g2(self.ctx))
 
+    def context_bytes(self) -> int:
+        """Device memory the context holds (hg_context_bytes)."""
+        return int(self.L.hg_context_bytes(self.ctx))
+
     def aggregate_tables(self) -> int:
         """Table level aggregate requests run at (hg_aggregate_tables): 0 = G2
         fold, 1 = GT fold over 8-key windows, 2 = over 16-key windows."""

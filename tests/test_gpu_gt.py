@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 from handel_amd._lib import HG_ERR_HASH_EOF, HandelGPUError
-from handel_amd.engine import REQ_DTYPE
+from handel_amd.engine import REQ_DTYPE, Engine
 from oracle import bn256_oracle as O
 from oracle import ref_lib as R
 from tests import _fixtures as F
@@ -104,6 +104,42 @@ def test_tables_follow_message_and_registry(engine):
                     assert (np.asarray(codes) == 0).sum() == 0
 
 
+def test_two_messages_keep_their_tables():
+    """Interleaved messages on ONE context: the context
+    caches the current and the previous message's hashedMessage and GT tables
+    (bn256/go/bn256.go:210-218: H, and every table, is fixed per message), so
+    alternating two messages stays at table level 2 with the oracle's
+    verdicts, and a table budget that holds one message's tables only drops
+    the other's."""
+    e = Engine(device=0, flavor="go")
+    try:
+        rng = np.random.default_rng(11)
+        ks = F.scalars(64, seed=b"two-msgs")
+        reg = R.g2_scalar_base(F.scalar_bytes(ks))
+        assert list(e.registry_load(reg)) == [0] * 64
+        msgs = [F.LIB_MESSAGE, F.TEST_MESSAGES[1]]
+        ranges = _levels(64, (3, 40))
+        batches = [_batch(ks, 64, m, ranges, rng) for m in msgs]
+        wants = [_oracle(m, reg, *b) for m, b in zip(msgs, batches)]
+        for m in msgs:
+            assert e.prepare_aggregate_msg(m) == 0
+        for i in range(6):
+            k = i % 2
+            codes = e.verify_aggregate_msg(msgs[k], *batches[k])
+            assert list(codes) == list(wants[k]), i
+            assert e.aggregate_tables() == 2, i
+        both = e.context_bytes()
+        # a budget for one message's level-2 tables: the cached message's go first
+        one = 64 // 16 * 65536 * 480 + 64 * 480 * 300
+        e.set_table_budget(one)
+        assert e.context_bytes() < both
+        assert e.aggregate_tables() == 2
+        codes = e.verify_aggregate_msg(msgs[1], *batches[1])
+        assert list(codes) == list(wants[1])
+    finally:
+        e.close()
+
+
 _CHILD = r"""
 import json, os, sys
 import numpy as np
@@ -157,9 +193,10 @@ def test_gt_and_g2_paths_agree():
 
 def test_volume_policy():
     """Without HG_GT_LEVEL: a message's first requests use the G2 fold, the
-    8-key GT tables appear once 16384 requests have come in, a new message
-    drops them, hg_prepare_aggregate builds the 16-key level — and the
-    verdicts are the same at every step."""
+    8-key GT tables appear once 16384 requests have come in, a switch to
+    another message and back keeps them (the context caches two messages),
+    a third message evicts them, hg_prepare_aggregate builds the 16-key level
+    — and the verdicts are the same at every step."""
     code = r"""
 import json, sys
 import numpy as np
@@ -179,7 +216,11 @@ for _ in range(5):
 run(1000, 2000)          # 17000: the 8-key tables
 assert e.set_message(b"Peaches and Cream") == 0
 assert e.set_message(bench.LIB_MESSAGE) == 0
-run(0, 100)              # tables dropped with the message change
+run(0, 100)              # the previous message's tables are kept
+assert e.set_message(b"Peaches and Cream") == 0
+assert e.set_message(b"Get Funky Tonight") == 0
+assert e.set_message(bench.LIB_MESSAGE) == 0
+run(0, 100)              # two other messages since: evicted
 assert e.prepare_aggregate() == 0
 run(0, 3000)
 print(json.dumps(out))
@@ -188,8 +229,8 @@ print(json.dumps(out))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert [ok for ok, _ in out] == [True] * 9
-    assert [lvl for _, lvl in out] == [0] * 6 + [1, 0, 2]
+    assert [ok for ok, _ in out] == [True] * 10
+    assert [lvl for _, lvl in out] == [0] * 6 + [1, 1, 0, 2]
 
 
 def test_sig_edge_cases_on_gt_path(engine):
