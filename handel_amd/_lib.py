@@ -57,6 +57,7 @@ _SZ = ctypes.c_size_t
 _I = ctypes.c_int
 SIGNATURES = {
     "hg_version": (_I, []),
+    "hg_context_flavor": (_I, [_P]),
     "hg_create": (_I, [_I, _I, ctypes.POINTER(_P)]),
     "hg_destroy": (None, [_P]),
     "hg_last_error": (ctypes.c_char_p, [_P]),

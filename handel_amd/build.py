@@ -22,7 +22,7 @@ DIAG_LIB = os.path.join(OUT_DIR, "libhandel_gpu_diag.so")
 SOURCES = ["bn256_verify.hip", "bn256_pair.hip", "bn256_kernels.hip", "bn256_gt.hip", "hg_api.cpp", "hg_batcher.cpp", "hg_packets.hip",
            "hg_service.cpp"]
 HEADERS = ["bn256_fp.h", "bn256_curve.h", "bn256_team.h", "bn256_kernels.h", "bn256_constants.h",
-           "bn256_g2team.h", "bn256_g2sched.h", "bn256_pairing.h", "bn256_xprog.h", "bn256_xtab.h", "bn256_inv.h", "bn256_agg.h", "bn256_gt.h", "bn256_decode.h", "hg_packets.h", "hg_shm.h"]
+           "bn256_g2team.h", "bn256_g2sched.h", "bn256_pairing.h", "bn256_xprog.h", "bn256_xtab.h", "bn256_inv.h", "bn256_agg.h", "bn256_gt.h", "bn256_decode.h", "hg_packets.h", "hg_shm.h", "hg_codes.h"]
 ARCH = os.environ.get("HG_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
@@ -81,7 +81,7 @@ def build_client(force: bool = False, verbose: bool = True) -> str:
     """libhandel_client.so: the verifier service's client side (hg_client.cpp,
     include/handel_client.h), host compiler only — no HIP runtime, so client
     processes never touch the GPU."""
-    srcs = [os.path.join(CSRC, "hg_client.cpp"), os.path.join(CSRC, "hg_shm.h"),
+    srcs = [os.path.join(CSRC, "hg_client.cpp"), os.path.join(CSRC, "hg_shm.h"), os.path.join(CSRC, "hg_codes.h"),
             os.path.join(HERE, "..", "include", "handel_client.h"), os.path.join(HERE, "..", "include", "handel_gpu.h"),
             os.path.abspath(__file__)]
     if not force and os.path.exists(CLIENT_LIB) and os.path.getmtime(CLIENT_LIB) >= max(map(os.path.getmtime, srcs)):
@@ -94,6 +94,24 @@ def build_client(force: bool = False, verbose: bool = True) -> str:
     subprocess.check_call(cmd)
     os.replace(tmp, CLIENT_LIB)
     return CLIENT_LIB
+
+
+VERIFIERD = os.path.join(OUT_DIR, "hg_verifierd")
+
+
+def build_verifierd(verbose: bool = True) -> str:
+    """hg_verifierd: the GPU-owning verifier process (hg_service_* over one
+    context) a single-host simul run starts once; links libhandel_gpu.so."""
+    src = os.path.join(CSRC, "hg_verifierd.cpp")
+    hdr = os.path.join(HERE, "..", "include", "handel_gpu.h")
+    if os.path.exists(VERIFIERD) and os.path.getmtime(VERIFIERD) >= max(map(os.path.getmtime, [src, hdr, LIB])):
+        return VERIFIERD
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", src, "-L", OUT_DIR, "-lhandel_gpu", "-lpthread",
+           "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib", "-Wl,-rpath,$ORIGIN", "-o", VERIFIERD]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return VERIFIERD
 
 
 ABI_THREADS = os.path.join(OUT_DIR, "abi_threads")
@@ -139,5 +157,6 @@ if __name__ == "__main__":
     print(build_library(force="--force" in sys.argv, diag="--diag" in sys.argv))
     if "--diag" not in sys.argv:
         print(build_client())
+        print(build_verifierd())
         print(build_native_tests())
         print(build_proxy())

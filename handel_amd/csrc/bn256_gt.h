@@ -10,6 +10,7 @@ struct Gt {
   uint32_t w[120];
 };
 static constexpr int kGtChunk = 8;  // default window-table values per fold chunk (one team)
+static constexpr int kGtChunkTeams = 5;  // k_gt_chunks: chunks per workgroup (five 12-lane teams)
 // The fold's windows: aligned 8-key windows (256 subset products each, 61 MB
 // for a 4000-key registry) or 16-key windows (65536 each, 7.9 GB, built from
 // the 8-key tables): GtWork.win_bits

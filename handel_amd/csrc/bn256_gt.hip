@@ -439,6 +439,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
 // count is on the device); every wave runs to the same, wave-uniform bound.
 // The next term is fetched from HBM into registers while the current product
 // runs.
+static_assert(kGtChunkTeams == kTeams12, "k_gt_chunks' teams per workgroup");
 __global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, const uint32_t* terms,
                                                   const int2* ord, int cap, const GtReq* plan, const GtHdr* hdr,
                                                   int chunk, Gt* partial, Gt* y) {

@@ -21,6 +21,7 @@
 
 #include "bn256_gt.h"
 #include "bn256_kernels.h"
+#include "hg_codes.h"
 #include "hg_packets.h"
 
 using namespace hg;
@@ -794,7 +795,10 @@ static int ensure_gt_fold(hg_ctx* c, Ws& ws, size_t n, const FoldCaps& caps, GtW
   w.cap = (int)caps.chunks;
   w.multi = ws.gt_multi.p;
   w.partial = ws.gt_partial.p;
-  w.chunk_grid = grid;
+  // no more chunk workgroups than the batch can have chunks (a small batch
+  // would otherwise launch thousands of workgroups that exit at once)
+  const size_t need = (caps.chunks + kGtChunkTeams - 1) / kGtChunkTeams;
+  w.chunk_grid = (int)(need < (size_t)grid ? (need ? need : 1) : (size_t)grid);
   w.chunk = gt_chunk();
   return HG_OK;
 }
@@ -1046,46 +1050,11 @@ extern "C" {
 
 int hg_version(void) { return 2; }
 
-const char* hg_code_string(int code, int flavor) {
-  switch (code) {
-    case HG_OK: return "";
-    case HG_ERR_SIG_INVALID: return "bn256: signature invalid";
-    case HG_ERR_HASH_EOF: return "EOF";
-    case HG_ERR_LEVEL: return "handel: inconsistent bitset with given level";
-    case HG_ERR_PK_UNMARSHAL: return "unable to unmarshal";
-    case HG_ERR_SIG_UNMARSHAL: return flavor == HG_FLAVOR_CF ? "bn256: multisig can't unmarshal: bn256: malformed point"
-                                                             : "bn256: multisig can't unmarshal";
-    case HG_ERR_EMPTY_AGG: return "runtime error: invalid memory address or nil pointer dereference";
-    case HG_ERR_CF_EXCEEDS: return "bn256: coordinate exceeds modulus";
-    case HG_ERR_CF_MALFORMED: return "bn256: malformed point";
-    case HG_ERR_CF_SHORT: return "bn256: not enough data";
-    case HG_ERR_SIG_CF_EXCEEDS: return "bn256: multisig can't unmarshal: bn256: coordinate exceeds modulus";
-    case HG_ERR_SIG_CF_MALFORMED: return "bn256: multisig can't unmarshal: bn256: malformed point";
-    case HG_ERR_SIG_CF_SHORT: return "bn256: multisig can't unmarshal: bn256: not enough data";
-    case HG_ERR_MULTI_SIZES: return "verify multisignature: inconsistent sizes";
-    case HG_ERR_PKT_ORIGIN: return "packet's origin out of range";
-    case HG_ERR_PKT_LEVEL: return "invalid packet's level";
-    case HG_ERR_PKT_EOF: return "EOF";
-    case HG_ERR_PKT_UNEXPECTED_EOF: return "unexpected EOF";
-    case HG_ERR_PKT_BITSET_SHORT: return "bitset received smaller than expected";
-    case HG_ERR_PKT_TYPE_MISMATCH: return "unmarshalling error: type mismatch";
-    case HG_ERR_PKT_BITSET_SIZE: return "invalid bitset's size for given level";
-    case HG_ERR_PKT_NO_SIG: return "no signature in the bitset";
-    case HG_ERR_PKT_ID_RANGE: return "globalID outside level's range";
-    case HG_PKT_NO_IND: return "";
-    case HG_ERR_ARG: return "invalid argument";
-    default: return "device error";
-  }
-}
+const char* hg_code_string(int code, int flavor) { return code_text(code, flavor); }
 
-const char* hg_processing_error_string(int code, int flavor) {
-  // processing.go:361-365 wraps only VerifySignature's error: fmt.Errorf("handel: %s", err)
-  switch (code) {
-    case HG_ERR_SIG_INVALID: return "handel: bn256: signature invalid";
-    case HG_ERR_HASH_EOF: return "handel: EOF";
-    default: return hg_code_string(code, flavor);
-  }
-}
+const char* hg_processing_error_string(int code, int flavor) { return processing_text(code, flavor); }
+
+int hg_context_flavor(hg_ctx* c) { return c ? c->flavor : -1; }
 
 const char* hg_last_error(hg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/handel_client.h"
+#include "hg_codes.h"
 #include "hg_shm.h"
 
 using namespace hgshm;
@@ -365,5 +366,15 @@ int hg_client_stats(hg_client* c, uint64_t* batches, uint64_t* requests) {
 }
 
 uint32_t hg_client_slot_bits(hg_client* c) { return c ? c->v.h->slot_words * 64u : 0; }
+
+int hg_client_flavor(hg_client* c) { return c ? (int)c->v.h->flavor : -1; }
+
+const char* hg_client_code_string(hg_client* c, int code) {
+  return hg::code_text(code, c ? (int)c->v.h->flavor : HG_FLAVOR_GO);
+}
+
+const char* hg_client_processing_error_string(hg_client* c, int code) {
+  return hg::processing_text(code, c ? (int)c->v.h->flavor : HG_FLAVOR_GO);
+}
 
 }  // extern "C"

@@ -60,18 +60,23 @@ struct GpuExec : Exec {
   explicit GpuExec(hg_ctx* c) : ctx(c) {}
   // one tiny batch per lane, waited for: every kernel of the path is loaded
   // and every lane's stream has run once before the first client's batch
+  // (all lanes at once: one pairing kernel's time); needs the context's
+  // message, else it waits for the first one
   void warm_up() {
+    bool ok = true;
     for (hg_lane* l : ln) {
       hg_request* r = nullptr;
       uint8_t* s = nullptr;
       uint64_t* w = nullptr;
-      if (hg_lane_stage(l, 1, 1, &r, &s, &w) != HG_OK) continue;
+      ok = ok && hg_lane_stage(l, 1, 1, &r, &s, &w) == HG_OK;
+      if (!ok) break;
       r[0] = hg_request{0, 1, 1, 0};
       w[0] = 1;
       memset(s, 0, 64);
-      if (hg_lane_submit(l) == HG_OK) (void)hg_lane_wait(l);
+      ok = hg_lane_submit(l) == HG_OK;
     }
-    warmed = true;
+    for (hg_lane* l : ln) (void)hg_lane_wait(l);
+    warmed = ok;
   }
   ~GpuExec() override {
     for (hg_lane* l : ln) hg_lane_destroy(l);
@@ -176,6 +181,7 @@ struct hg_service {
   uint64_t msg_requests = 0;
   int built_level = 0;
   uint64_t max_in_flight = 0;
+  Clock::time_point last_arrival;
   std::vector<uint32_t> take;
 
   bool intake();
@@ -205,6 +211,7 @@ bool hg_service::intake() {
       any = true;
     }
   }
+  if (any) last_arrival = now;
   return any;
 }
 
@@ -349,6 +356,7 @@ void hg_service::launch(int lane) {
 
 void hg_service::run() {
   const auto linger = std::chrono::microseconds(cfg.max_wait_us);
+  const auto quiet = std::chrono::microseconds(cfg.quiet_us);
   Header* h = v.h;
   for (;;) {
     bool progress = false;
@@ -368,8 +376,11 @@ void hg_service::run() {
         if (!lanes[i].busy) free_lane = i;
       if (free_lane < 0) break;
       const bool full = pending.size() >= cfg.max_batch;
-      const bool old = Clock::now() - pending.front().seen >= linger;
-      if (!full && !old && !stopping) break;
+      const auto now = Clock::now();
+      const bool old = now - pending.front().seen >= linger;
+      // a burst of resubmissions (the clients of a finished batch) has ended
+      const bool calm = cfg.quiet_us && now - last_arrival >= quiet;
+      if (!full && !old && !calm && !stopping) break;
       launch(free_lane);
       progress = true;
     }
@@ -470,6 +481,7 @@ void hg_service_config_init(hg_service_config* c) {
   c->lanes = 8;
   c->max_batch = 4096;
   c->max_wait_us = 50;
+  c->quiet_us = 0;
   c->prepare = 1;
   c->overlap = 1;
 }
@@ -479,7 +491,7 @@ int hg_service_create(hg_ctx* ctx, const char* name, const hg_service_config* cf
   const size_t nreg = hg_registry_size(ctx);
   if (nreg == 0 || nreg > UINT32_MAX) return HG_ERR_ARG;
   hg_service* s = nullptr;
-  int rc = create_common(name, cfg, (uint32_t)nreg, 0, out, s);
+  int rc = create_common(name, cfg, (uint32_t)nreg, (uint32_t)hg_context_flavor(ctx), out, s);
   if (rc) return rc;
   GpuExec* g = new GpuExec(ctx);
   const size_t max_words = (size_t)s->cfg.max_batch * s->v.h->slot_words;
@@ -498,6 +510,7 @@ int hg_service_create(hg_ctx* ctx, const char* name, const hg_service_config* cf
     return rc;
   }
   s->ex = g;
+  g->warm_up();  // under the context's current message, if it has one
   start(s);
   *out = s;
   return HG_OK;

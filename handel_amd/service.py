@@ -29,6 +29,7 @@ class ServiceConfig(ctypes.Structure):
     """hg_service_config."""
     _fields_ = [("slots", ctypes.c_uint32), ("slot_bits", ctypes.c_uint32), ("channels", ctypes.c_uint32),
                 ("lanes", ctypes.c_uint32), ("max_batch", ctypes.c_uint32), ("max_wait_us", ctypes.c_uint32),
+                ("quiet_us", ctypes.c_uint32),
                 ("prepare", ctypes.c_int32), ("overlap", ctypes.c_int32)]
 
 
@@ -122,6 +123,9 @@ CLIENT_SIGNATURES = {
     "hg_client_verify_aggregate": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _P, ctypes.POINTER(ctypes.c_int32)]),
     "hg_client_stats": (ctypes.c_int, [_P, _P, _P]),
     "hg_client_slot_bits": (ctypes.c_uint32, [_P]),
+    "hg_client_flavor": (ctypes.c_int, [_P]),
+    "hg_client_code_string": (ctypes.c_char_p, [_P, ctypes.c_int]),
+    "hg_client_processing_error_string": (ctypes.c_char_p, [_P, ctypes.c_int]),
 }
 _client_lock = threading.Lock()
 _client_lib = None
@@ -231,6 +235,17 @@ class Client:
         b, r = ctypes.c_uint64(), ctypes.c_uint64()
         self.L.hg_client_stats(self.h, ctypes.byref(b), ctypes.byref(r))
         return b.value, r.value
+
+    @property
+    def flavor(self) -> int:
+        return int(self.L.hg_client_flavor(self.h))
+
+    def code_string(self, code: int) -> str:
+        return self.L.hg_client_code_string(self.h, int(code)).decode()
+
+    def processing_error_string(self, code: int) -> str:
+        """processing.go verifySignature's text for a code (None-equivalent "" for HG_OK)."""
+        return self.L.hg_client_processing_error_string(self.h, int(code)).decode()
 
 
 def service_name(tag: Optional[str] = None) -> str:

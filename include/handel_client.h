@@ -56,6 +56,13 @@ int hg_client_verify_aggregate(hg_client* cl, const uint8_t* msg, size_t len, co
 int hg_client_stats(hg_client* cl, uint64_t* batches, uint64_t* requests);
 /* The region's largest bitset per request, in bits. */
 uint32_t hg_client_slot_bits(hg_client* cl);
+/* The service context's flavor, and the reference's texts for a code under
+ * it: hg_code_string's and hg_processing_error_string's (processing.go:342-368:
+ * VerifySignature's errors wrapped "handel: <err>"), without linking the GPU
+ * library. */
+int hg_client_flavor(hg_client* cl);
+const char* hg_client_code_string(hg_client* cl, int code);
+const char* hg_client_processing_error_string(hg_client* cl, int code);
 
 #ifdef __cplusplus
 }

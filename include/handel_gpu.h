@@ -96,6 +96,8 @@ const char* hg_code_string(int code, int flavor);
  * everything else as hg_code_string. "" for HG_OK. */
 const char* hg_processing_error_string(int code, int flavor);
 int hg_version(void);
+/* The context's flavor (HG_FLAVOR_GO / HG_FLAVOR_CF), -1 for NULL. */
+int hg_context_flavor(hg_ctx* ctx);
 
 /* Registry.Identities(...).PublicKey() source: uploads n marshalled G2
  * public keys (PublicKey.UnmarshalBinary, bn256/go/bn256.go:113-120), decoding
@@ -401,6 +403,7 @@ typedef struct {
   uint32_t lanes;       /* batches in flight on the GPU (default 8) */
   uint32_t max_batch;   /* requests per batch (default 4096) */
   uint32_t max_wait_us; /* a queued request waits at most this long for more to batch with (default 50) */
+  uint32_t quiet_us;    /* ... or until no request has arrived for quiet_us (0 = off; the default) */
   int32_t prepare;      /* 1 (default): a message's first batch builds its top GT table level;
                            0: the context's volume policy (levels 1 and 2 after 16384 / 2^20 requests) */
   int32_t overlap;      /* 1 (default): the GT fold beside the pairing kernel inside each lane */
