@@ -43,7 +43,8 @@ struct GtWork {
   int cap;         // entries of ord and partial
   Gt* partial;
   int* multi;      // 2n: the big requests from 0, the mid ones from n (k_gt_combine's order)
-  int chunk_grid;  // workgroups of k_gt_chunks (4 teams each)
+  int chunk_grid;  // workgroups of k_gt_chunks (one wave: kGtChunkTeams teams, or 10 with k6)
+  int k6;          // the 6-lane Karatsuba kernels (k_gt_chunks6 / k_gt_combine6)
   int chunk;       // terms per chunk
   int win_bits;    // 8 or 16: which window table `win` is
 };

@@ -17,7 +17,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GO = os.path.join(ROOT, "go")
-HEADER = open(os.path.join(ROOT, "include", "handel_gpu.h")).read()
+HEADER = (open(os.path.join(ROOT, "include", "handel_gpu.h")).read() +
+          open(os.path.join(ROOT, "include", "handel_client.h")).read())
 
 
 def _go_sources():
@@ -32,7 +33,7 @@ def _go_sources():
 def test_go_files_present():
     src = _go_sources()
     for f in ("bn256/hip/engine.go", "bn256/hip/bn256.go", "bn256/hip/batcher.go", "bn256/hip/registry.go",
-              "bn256/hip/bn256_test.go", "handel/batched_processing.go"):
+              "bn256/hip/bn256_test.go", "handel/batched_processing.go", "bn256/hipsvc/client.go"):
         assert f in src, f
     assert os.path.exists(os.path.join(GO, "handel", "config_hook.patch"))
 
@@ -43,7 +44,7 @@ def test_cgo_identifiers_declared_in_header():
         used |= set(re.findall(r"\bC\.(hg_\w+|HG_\w+)", text))
     assert used, "the cgo binding uses the C ABI"
     for name in sorted(used):
-        assert re.search(r"\b%s\b" % name, HEADER), f"{name} not declared in include/handel_gpu.h"
+        assert re.search(r"\b%s\b" % name, HEADER), f"{name} not declared in include/handel_gpu.h or handel_client.h"
 
 
 def test_cgo_functions_exported_by_library():
@@ -52,12 +53,14 @@ def test_cgo_functions_exported_by_library():
     if not os.path.exists(B.LIB):
         pytest.skip("library not built")
     lib = ctypes.CDLL(B.LIB)
-    funcs = set()
-    for text in _go_sources().values():
-        funcs |= set(re.findall(r"\bC\.(hg_[a-z0-9_]+)\(", text))
-    funcs.discard("hg_request")
-    for f in sorted(funcs):
-        assert hasattr(lib, f), f
+    client = ctypes.CDLL(B.build_client(verbose=False))
+    for name, text in _go_sources().items():
+        funcs = set(re.findall(r"\bC\.(hg_[a-z0-9_]+)\(", text))
+        funcs.discard("hg_request")
+        # the service client package links libhandel_client.so only (no GPU runtime)
+        target = client if name.startswith("bn256/hipsvc/") else lib
+        for f in sorted(funcs):
+            assert hasattr(target, f), (name, f)
 
 
 def test_go_expected_error_texts_match_abi():
