@@ -24,6 +24,7 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"math"
 	"sync"
 	"unsafe"
 )
@@ -488,6 +489,11 @@ func (e *Engine) ParsePackets(receivers []int, pkts []Packet) ([]ParsedPacket, e
 	var pool []byte
 	recs := make([]C.hg_packet, n)
 	for i, p := range pkts {
+		// pool offsets and lengths are 32-bit in hg_packet: a batch whose pool
+		// would pass 4 GiB is refused instead of wrapping into wrong bytes
+		if uint64(len(pool))+uint64(len(p.MultiSig))+uint64(len(p.IndividualSig)) > math.MaxUint32 {
+			return nil, &DeviceError{Code: C.HG_ERR_ARG, Msg: "ParsePackets: the batch's packets exceed 4 GiB; split it"}
+		}
 		recs[i] = C.hg_packet{origin: C.int32_t(p.Origin), receiver: C.uint32_t(receivers[i]),
 			level: C.uint32_t(p.Level), ms_off: C.uint32_t(len(pool)), ms_len: C.uint32_t(len(p.MultiSig))}
 		pool = append(pool, p.MultiSig...)

@@ -27,6 +27,8 @@
 // waves share a SIMD, also beside k_verify_sig's waves.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "bn256_agg.h"
 #include "bn256_decode.h"
 #include "bn256_gt.h"
@@ -240,6 +242,39 @@ __global__ __launch_bounds__(64) void k_gt_win16(const Gt* w8, int nwin8, int nw
     team_sync();
     if (valid) gt_store(T, S_A, dst + lo);
   }
+}
+
+// The same on 6-lane Karatsuba teams (bn256_k6.h): ten (window, hi) tasks per
+// wave; the hi value is the right factor of all 256 products, put once.
+__global__ __launch_bounds__(64, 2) void k_gt_win16_6(const Gt* w8, int nwin8, int nwin16, Gt* w16) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams6 * kT6Words];
+  const Team6 T = make_team6(lds);
+  const int task = blockIdx.x * kTeams6 + team6_index();
+  const bool valid = task < 256 * nwin16;
+  const int w = valid ? task >> 8 : 0, hi = task & 255;
+  const Gt* lo_tab = w8 + (size_t)(2 * w) * 256;
+  const bool has_hi = 2 * w + 1 < nwin8;
+  Gt* dst = w16 + (size_t)w * 65536 + (size_t)hi * 256;
+  Fp hx, hy, nx, ny;
+  k6_read(hx, hy, w8 + (size_t)(has_hi ? 2 * w + 1 : 2 * w) * 256 + hi, T);
+  k6_keep_or_one(hx, hy, has_hi, T);
+  k6_put_b(T, hx, hy, false);
+  k6_read(nx, ny, lo_tab, T);
+#pragma unroll 1
+  for (int lo = 0; lo < 256; lo++) {
+    k6_put_a(T, nx, ny, false);
+    if (lo + 1 < 256) k6_read(nx, ny, lo_tab + lo + 1, T);
+    k6_mul(T);
+    if (valid) k6_store(T, dst + lo);
+  }
+}
+
+bool gt_k6() {
+  static const bool on = [] {
+    const char* e = getenv("HG_GT_K6");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // Block products, one level: dst[j] = src[2j] * src[2j + 1] (the last block of
@@ -852,7 +887,9 @@ void launch_gt_windows8(const Gt* key, int nreg, Gt* w8, int nwin8, hipStream_t 
   k_gt_cross<<<nblk(15 * nwin8, 4), 64, 0, s>>>(nwin8, w8);
 }
 void launch_gt_windows16(const Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s) {
-  if (nwin16 > 0) k_gt_win16<<<nblk(256 * nwin16, kTeams12), 64, 0, s>>>(w8, nwin8, nwin16, w16);
+  if (nwin16 <= 0) return;
+  if (gt_k6()) k_gt_win16_6<<<nblk(256 * nwin16, kTeams6), 64, 0, s>>>(w8, nwin8, nwin16, w16);
+  else k_gt_win16<<<nblk(256 * nwin16, kTeams12), 64, 0, s>>>(w8, nwin8, nwin16, w16);
 }
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s) {
   if (ndst > 0) k_gt_blocks<<<nblk(ndst, 4), 64, 0, s>>>(src, stride, nsrc, dst, ndst);

@@ -796,7 +796,7 @@ static int ensure_gt_fold(hg_ctx* c, Ws& ws, size_t n, const FoldCaps& caps, GtW
   w.multi = ws.gt_multi.p;
   w.partial = ws.gt_partial.p;
   // the 6-lane Karatsuba fold (bn256_k6.h) unless HG_GT_K6=0 (A/B runs)
-  static const int k6 = env_int("HG_GT_K6", 1, 0, 1);
+  const int k6 = gt_k6() ? 1 : 0;
   w.k6 = k6;
   const size_t per_wg = k6 ? 10 : kGtChunkTeams;
   // no more chunk workgroups than the batch can have chunks (a small batch
