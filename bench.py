@@ -641,6 +641,32 @@ def batch_latency(eng: Engine, head, dev, sizes=(32, 128, 512, 4096), reps: int 
     return out
 
 
+def config4_proxy(model: str, timeout: int = 180):
+    """Config 4's verification load in simul's single-host process layout
+    (tests/native/handel_proxy.c): 8 processes x 250 Handel instances x 45
+    checks on a 2000-key registry, one check in flight per instance, every
+    verdict checked against the expected one. model 'service': one GPU-owning
+    verifier process (hg_service_*, 8 lanes) and 8 client processes that load
+    only libhandel_client.so; 'contexts': every process its own context, GT
+    tables and batcher (the r03 layout). Not Handel completion time."""
+    import subprocess
+
+    from handel_amd import build as B
+
+    args = ["-D", "1", "-P", "1", "-l", "8"] if model == "service" else ["-D", "0", "-P", "1"]
+    try:
+        r = subprocess.run([B.HANDEL_PROXY, B.LIB, *args], capture_output=True, text=True, timeout=timeout)
+    except (OSError, subprocess.TimeoutExpired) as e:  # pragma: no cover - reported, not fatal
+        return {"error": str(e)}
+    if r.returncode != 0:
+        return {"error": f"rc {r.returncode}: {r.stderr[-500:]}"}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    keep = ("model", "procs", "instances_per_proc", "registry", "checks_per_instance", "lanes", "hw_queues",
+            "requests", "batches", "mean_batch", "wall_ms", "throughput", "latency_us", "hbm_total_bytes",
+            "contexts", "mismatches")
+    return {k: d[k] for k in keep if k in d}
+
+
 def timed_phases(eng: Engine, run):
     """Runs run() with the engine's HIP-event timing on; returns per-phase
     (mean ms per interval) for verify / aggregate fold / whole submission."""
@@ -689,6 +715,7 @@ def main():
     ap.add_argument("--pipeline-overlap", type=int, default=1,
                     help="the pipelined line's contexts run their fold beside the pairing kernel (1) or before it (0)")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="requests in the CPU baseline's sample")
+    ap.add_argument("--no-service", action="store_true", help="skip the config-4 process-model lines")
     ap.add_argument("--prewarm", type=float, default=0.3,
                     help="seconds of untimed headline steps before the warmup steps (GPU clocks settle)")
     args = ap.parse_args()
@@ -899,6 +926,11 @@ def main():
                     "per-check latency floor a one-check-at-a-time evaluator (processing.go:228-287) sees",
             **batch_latency(eng, head, dev)}
         extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)
+        if rank == 0 and world == 1 and not args.no_service:
+            extra["config4_proxy"] = {
+                "what": "simul's 2000-node single-host verification load (8 processes x 250 instances x 45 checks, "
+                        "one check in flight per instance) on this GPU; checks/s, per-check latency, HBM",
+                "service": config4_proxy("service"), "contexts": config4_proxy("contexts")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
