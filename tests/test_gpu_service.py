@@ -118,3 +118,35 @@ def test_proxy_daemon_verdicts_match_oracle(tmp_path, level, lanes):
                               reqs["word_offset"].astype(np.uint64), sigs, nthreads=8)
     assert np.array_equal(got, want)
     assert (got == 1).sum() == (len(got) + 7) // 8
+
+
+def test_verifierd_serves_registry_file(tmp_path, reg300):
+    """hg_verifierd with --registry/--message (the daemon a simul host starts):
+    tables built before "ready", verdicts through a client equal the oracle's,
+    SIGTERM prints the statistics and exits 0."""
+    import signal
+
+    ks, pks = reg300
+    (tmp_path / "reg.bin").write_bytes(pks)
+    (tmp_path / "msg.bin").write_bytes(F.LIB_MESSAGE)
+    rng = np.random.default_rng(11)
+    reqs, words, sigs = _batch(ks, NREG, F.LIB_MESSAGE, _levels(NREG, rng.integers(0, NREG, size=8)) * 4, rng)
+    want = _oracle(F.LIB_MESSAGE, pks, reqs, words, sigs)
+    name = service_name("vdgpu")
+    exe = B.build_verifierd(verbose=False)
+    p = subprocess.Popen([exe, "--name", name, "--registry", str(tmp_path / "reg.bin"), "--message",
+                          str(tmp_path / "msg.bin"), "--lanes", "3"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True)
+    try:
+        ready = json.loads(p.stdout.readline() or "{}")
+        assert ready.get("ready") == name and ready["registry"] == NREG and ready["tables"] == 2, p.stderr.read()
+        with Client(name) as cl:
+            assert cl.flavor() == 0
+            got = cl.verify_many(F.LIB_MESSAGE, reqs, words, sigs)
+        assert np.array_equal(got, want)
+    finally:
+        p.send_signal(signal.SIGTERM)
+        out, err = p.communicate(timeout=60)
+    assert p.returncode == 0, err
+    stats = json.loads(out.strip().splitlines()[-1])
+    assert stats["requests"] == len(reqs) and stats["tables"] == 2

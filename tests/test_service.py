@@ -189,3 +189,47 @@ def test_proxy_many_processes_over_the_echo_service(procs, pollers):
     assert out["model"] == "daemon-echo" and out["mismatches"] == 0
     assert out["requests"] == procs * 40 * 6
     assert out["batches"] < out["requests"]
+
+
+def _start_verifierd(args):
+    exe = B.build_verifierd(verbose=False)
+    p = subprocess.Popen([exe, *args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    line = p.stdout.readline()
+    assert line, p.stderr.read()
+    return p, json.loads(line)
+
+
+def test_verifierd_echo_serves_until_sigterm():
+    """hg_verifierd: the daemon a single-host run starts once; SIGTERM verifies
+    what is queued, prints its statistics and exits 0."""
+    import signal
+
+    name = service_name("vd")
+    p, ready = _start_verifierd(["--name", name, "--echo", "50", "--nreg", "400", "--lanes", "2"])
+    try:
+        assert ready["ready"] == name and ready["registry"] == 400
+        with Client(name) as cl:
+            rng = np.random.default_rng(5)
+            want, tickets = [], []
+            for _ in range(64):
+                off, size, w, sig, exp = _req(rng, 400, [])
+                tickets.append(cl.submit(MSG, off, size, size, w, sig))
+                want.append(exp)
+            assert [cl.wait(t) for t in tickets] == want
+            assert cl.processing_error_string(1) == "handel: bn256: signature invalid"
+            assert cl.code_string(3) == "handel: inconsistent bitset with given level"
+    finally:
+        p.send_signal(signal.SIGTERM)
+        out, err = p.communicate(timeout=30)
+    assert p.returncode == 0, err
+    stats = json.loads(out.strip().splitlines()[-1])
+    assert stats["stopped"] == name and stats["requests"] == 64
+
+
+def test_verifierd_rejects_bad_arguments(tmp_path):
+    exe = B.build_verifierd(verbose=False)
+    assert subprocess.run([exe], capture_output=True).returncode == 2
+    bad = tmp_path / "reg.bin"
+    bad.write_bytes(bytes(100))  # not a multiple of 128
+    r = subprocess.run([exe, "--name", service_name("vd2"), "--registry", str(bad)], capture_output=True, text=True)
+    assert r.returncode == 2 and "128-byte" in r.stderr
