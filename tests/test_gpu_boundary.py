@@ -349,3 +349,41 @@ def test_native_batcher_two_messages_threads(engine):
     for k in range(2):
         assert np.array_equal(got[k], want[k]), k
     assert requests == 2 * n and batches < requests
+
+
+def test_native_batcher_close_while_waiting(engine):
+    """hg_batcher_destroy verifies every queued ticket before it returns and
+    tickets hold their own state: threads blocked in wait while another thread
+    closes the batcher, and waits made after the close, all get their verdicts;
+    a submit after the close is refused."""
+    import threading
+
+    import bench
+    from handel_amd.engine import Batcher, HandelGPUError
+
+    assert engine.set_message(bench.LIB_MESSAGE) == 0
+    reqs, words, sigs, expect, _, _ = bench.make_aggregate_batch(engine, 300, 48, seed=37)
+    b = Batcher(engine, max_batch=16, max_wait_us=20000)  # a long linger: the close finds tickets queued
+    tickets = []
+    for i in range(len(reqs)):
+        r = reqs[i]
+        nw = (int(r["bitlen"]) + 63) // 64
+        tickets.append(b.submit(bench.LIB_MESSAGE, int(r["offset"]), int(r["bitlen"]), int(r["level_size"]),
+                                words[int(r["word_offset"]):int(r["word_offset"]) + nw], sigs[64 * i:64 * i + 64]))
+    got = np.full(len(reqs), -1, dtype=np.int32)
+
+    def waiter(k):
+        for i in range(k, 24, 4):
+            got[i] = b.wait(tickets[i])
+
+    ths = [threading.Thread(target=waiter, args=(k,)) for k in range(4)]
+    for th in ths:
+        th.start()
+    b.close()  # while the waiters block
+    for i in range(24, len(reqs)):  # collected after the batcher is gone
+        got[i] = b.wait(tickets[i])
+    for th in ths:
+        th.join(60)
+    assert np.array_equal(got, expect)
+    with pytest.raises(HandelGPUError):
+        b.submit(bench.LIB_MESSAGE, 0, 0, 1, np.zeros(0, dtype=np.uint64), bytes(64))
