@@ -10,9 +10,17 @@
 // with each Fp2 product u v as three Fp products (Karatsuba):
 //     t0 = u.y v.y, t1 = u.x v.x, t2 = (u.x + u.y)(v.x + v.y)
 //     re = t0 - t1,  im = t2 - t0 - t1
-// accumulated over the six terms in three lazy column sums T0, T1, T2 and
-// reduced twice: 108 Fp products per Fp12 product, and ten teams per wave
-// instead of five, so about a fifth fewer lane-instructions per product.
+// summed over the six terms as lazy 64-bit column sums T0, T1, T2 and reduced
+// twice: 108 Fp products per Fp12 product, and ten teams per wave instead of
+// five, so about a fifth fewer lane-instructions per product.
+//
+// Registers: the fold runs beside the pairing kernel (264 registers a wave),
+// so a fold wave must stay within the other 248 of the SIMD's 512. The sums
+// run in two passes: T0 and T1 (two accumulators) over the six terms, then
+// re = T0 - T1 is reduced and the second accumulator restarts from -(T0 + T1)
+// and takes T2. The operand sums u.x + u.y, v.x + v.y are stored beside the
+// operands when they are written (slots SA, SX, SB), so pass 2 reads two
+// elements per term.
 //
 // Exactness: every partial product goes into 64-bit columns with no carries.
 // im's columns T2 - T0 - T1 are those of sum(u.x v.y + u.y v.x) >= 0, so the
@@ -44,9 +52,11 @@ static constexpr uint32_t kP4L[10] = {0x0422599cu, 0x04ac6c5du, 0x05678616u, 0x0
 // Ten 6-lane teams per wave (lanes 6 t .. 6 t + 5; lanes 60..63 idle, team 9's).
 static constexpr int kTeams6 = 10;
 // Team region: A (12 elements: the running product), B (12: the factor),
-// X (12: xi A_k lazily, coefficient 0 unused) — element e = 2k + c at 10 e.
-static constexpr int kT6Words = 3 * kFp12Words;
+// X (12: xi A_k lazily, coefficient 0 unused) — element e = 2k + c at 10 e —
+// then the sums x + y of A's, B's and X's six coefficients (6 elements each).
+static constexpr int kT6Words = 3 * kFp12Words + 3 * 60;
 enum { K6_A = 0, K6_B = 1, K6_X = 2 };
+enum { K6_SA = 0, K6_SB = 1, K6_SX = 2 };
 
 struct Team6 {
   uint32_t* base;
@@ -70,6 +80,7 @@ HG_DEV Team6 make_team6(uint32_t* lds_base) {
   return T;
 }
 HG_DEV uint32_t* k6_slot(const Team6& T, int s) { return T.base + s * kFp12Words; }
+HG_DEV uint32_t* k6_sums(const Team6& T, int s) { return T.base + 3 * kFp12Words + s * 60; }
 
 HG_DEV void acc_init_k6c(Acc& a) {
 #pragma unroll
@@ -77,38 +88,42 @@ HG_DEV void acc_init_k6c(Acc& a) {
   a.c[19] = a.c[20] = 0;
 }
 
-// three independent Karatsuba column sums of one Fp2 product, interleaved
-HG_DEV void k6_term(Acc& a0, Acc& a1, Acc& a2, const Fp& ux, const Fp& uy, const Fp& vx, const Fp& vy) {
-  uint32_t sv[10];
+// acc += x y, each partial product one v_mad_u64_u32 into its column (the
+// empty asm keeps LLVM from re-associating a column into a serial chain)
+HG_DEV void acc_mad_pinned6(Acc& a, const Fp& x, const Fp& y) {
 #pragma unroll
-  for (int l = 0; l < 10; l++) sv[l] = vx.l[l] + vy.l[l];
+  for (int i = 0; i < 10; i++)
 #pragma unroll
-  for (int i = 0; i < 10; i++) {
-    const uint32_t su = ux.l[i] + uy.l[i];
+    for (int j = 0; j < 10; j++) {
+      a.c[i + j] += (uint64_t)x.l[i] * y.l[j];
+      asm("" : "+v"(a.c[i + j]));
+    }
+}
+
+// pass 1: T0 += u.y v.y, T1 += u.x v.x (two independent chains, interleaved)
+HG_DEV void k6_term01(Acc& a0, Acc& a1, const Fp& ux, const Fp& uy, const Fp& vx, const Fp& vy) {
+#pragma unroll
+  for (int i = 0; i < 10; i++)
 #pragma unroll
     for (int j = 0; j < 10; j++) {
       a0.c[i + j] += (uint64_t)uy.l[i] * vy.l[j];
       asm("" : "+v"(a0.c[i + j]));
       a1.c[i + j] += (uint64_t)ux.l[i] * vx.l[j];
       asm("" : "+v"(a1.c[i + j]));
-      a2.c[i + j] += (uint64_t)su * sv[j];
-      asm("" : "+v"(a2.c[i + j]));
     }
-  }
 }
 
-// lane k's coefficient of A * B into (cx, cy), canonical; reads A, X, B.
-// Several fold waves share a SIMD, so the operand loads are not prefetched
-// (the registers go to the three accumulators instead).
+// lane k's coefficient of A * B into (cx, cy), canonical; reads A, X, B and
+// their sums. Several fold waves share a SIMD, so the operand loads are not
+// prefetched (the registers stay free for a wave beside the pairing kernel).
+// term i: u = A_i (i <= k) or xi A_i (i > k: wraps past w^6), v = B_(k - i mod 6)
 HG_DEV void k6_coeff(const Team6& T, Fp& cx, Fp& cy) {
-  Acc a0, a1, a2;
+  Acc a0, a1;
   acc_init_k6c(a0);
   acc_zero(a1);
-  acc_zero(a2);
   const uint32_t* A = k6_slot(T, K6_A);
   const uint32_t* X = k6_slot(T, K6_X);
   const uint32_t* B = k6_slot(T, K6_B);
-  // term i: u = A_i (i <= k) or xi A_i (i > k: wraps past w^6), v = B_(k - i mod 6)
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     const uint32_t* u = (i <= T.k ? A : X) + 20 * i;
@@ -118,18 +133,30 @@ HG_DEV void k6_coeff(const Team6& T, Fp& cx, Fp& cy) {
     ld_fp_a8(uy, u + 10);
     ld_fp_a8(vx, v);
     ld_fp_a8(vy, v + 10);
-    k6_term(a0, a1, a2, ux, uy, vx, vy);
+    k6_term01(a0, a1, ux, uy, vx, vy);
     __builtin_amdgcn_sched_barrier(0);
   }
-  // re = T0 + C - T1 (a0 holds T0 + C), im = T2 - T0 - T1 = a2 - a0 - a1 + C
+  // re = T0 + C - T1 (a0 holds T0 + C); a1 restarts at -(T0 + T1) mod 2^64
 #pragma unroll
   for (int c = 0; c < 19; c++) {
-    const uint64_t t01 = a0.c[c] - a1.c[c];
-    a2.c[c] = a2.c[c] - a0.c[c] - a1.c[c] + kK6C[c];
-    a0.c[c] = t01;
+    const uint64_t t0c = a0.c[c], t1 = a1.c[c];
+    a0.c[c] = t0c - t1;
+    a1.c[c] = kK6C[c] - t0c - t1;
   }
   acc_reduce(cy, a0);
-  acc_reduce(cx, a2);
+  // pass 2: im = T2 - T0 - T1, T2 = sum (u.x + u.y)(v.x + v.y)
+  const uint32_t* SA = k6_sums(T, K6_SA);
+  const uint32_t* SX = k6_sums(T, K6_SX);
+  const uint32_t* SB = k6_sums(T, K6_SB);
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    Fp su, sv;
+    ld_fp_a8(su, (i <= T.k ? SA : SX) + 10 * i);
+    ld_fp_a8(sv, SB + 10 * ((T.k - i + 6) % 6));
+    acc_mad_pinned6(a1, su, sv);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  acc_reduce(cx, a1);
 }
 
 // lane k stores its coefficient into A and xi times it into X:
@@ -144,10 +171,18 @@ HG_DEV void k6_put(const Team6& T, const Fp& cx, const Fp& cy) {
     xx[l] = 3 * cx.l[l] + cy.l[l];
     xy[l] = 3 * cy.l[l] + kP4L[l] - cx.l[l];
   }
+  uint32_t sa[10], sx[10];
+#pragma unroll
+  for (int l = 0; l < 10; l++) {
+    sa[l] = cx.l[l] + cy.l[l];
+    sx[l] = xx[l] + xy[l];
+  }
   st_fp_a8(A, cx.l);
   st_fp_a8(A + 10, cy.l);
   st_fp_a8(X, xx);
   st_fp_a8(X + 10, xy);
+  st_fp_a8(k6_sums(T, K6_SA) + 10 * T.k, sa);
+  st_fp_a8(k6_sums(T, K6_SX) + 10 * T.k, sx);
 }
 
 // A = A * B (then X = xi A): every lane's reads of A and X are done before
@@ -200,8 +235,12 @@ HG_DEV void k6_put_b(const Team6& T, Fp x, Fp y, bool conj) {
   }
   if (!T.active) return;
   uint32_t* B = k6_slot(T, K6_B) + 20 * T.k;
+  uint32_t sb[10];
+#pragma unroll
+  for (int l = 0; l < 10; l++) sb[l] = x.l[l] + y.l[l];
   st_fp_a8(B, x.l);
   st_fp_a8(B + 10, y.l);
+  st_fp_a8(k6_sums(T, K6_SB) + 10 * T.k, sb);
 }
 // into slot A (and X = xi A), for the first factor of a product chain
 HG_DEV void k6_put_a(const Team6& T, Fp x, Fp y, bool conj) {
