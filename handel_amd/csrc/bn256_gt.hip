@@ -808,7 +808,7 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
   // second batch's pairing waves (two contexts in flight) share SIMDs and
   // crowd the fold's workgroups out of the CU's LDS; marking v255 and one
   // AGPR used makes its allocation exceed half of the 512-entry file
-  asm volatile("" ::: "v255", "a0");
+  if constexpr (TEAMS == 4) asm volatile("" ::: "v255", "a0");
   Team T = make_team(lds, kSigTeamWords);
   uint32_t* F = team_regs(T);
   const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
@@ -915,8 +915,19 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
   if (n > 0) k_verify_sig<4, false><<<nblk(n, 4), 64, 0, s>>>(sigs, nullptr, 0, n, tab, y, nullptr, codes);
 }
+// HG_SIG_TEAMS=2 (experiment): two checks per wave and no register padding,
+// so two pairing waves share each SIMD at a 4096 batch
+static int sig_teams() {
+  static const int t = [] {
+    const char* e = getenv("HG_SIG_TEAMS");
+    return e && atoi(e) == 2 ? 2 : 4;
+  }();
+  return t;
+}
 void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
-  if (n > 0) k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
+  if (n <= 0) return;
+  if (sig_teams() == 2) k_verify_sig<2, true><<<nblk(n, 2), 32, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
+  else k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
 }
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s) {
   if (n > 0) k_gt_compare<<<n, 64, 0, s>>>(fe, y, n, codes);
