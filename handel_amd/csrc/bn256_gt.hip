@@ -701,10 +701,11 @@ __global__ __launch_bounds__(64) void k_gt_combine6(int n, const GtHdr* hdr, con
 //
 // The table's lines are normalised (k_g2_lines: c' + b' w + w^3), so f * line
 // is 4 products per lane plus the w^3 shift as a linear term.
-using ISdbl = XInst<XP_SDBL, S_F, S_F>;
-using ILfev = XInst<XP_LFEV, S_F, S_F>;
-using IFeval = XInst<XP_FEVAL>;
-using ILfix = XInst<XP_LINE_FIX, S_F, S_F>;
+// (layout S: k_verify_sig's compact team region, see team_final_exp_fc_s)
+using ISdbl = XInst<XP_SDBL_S, S_F, S_F>;
+using ILfev = XInst<XP_LFEV_S, S_F, S_F>;
+using IFeval = XInst<XP_FEVAL_S>;
+using ILfix = XInst<XP_LINE_FIX_S, S_F, S_F>;
 
 // The G2Base lines reach the team's registers through one VGPR element per
 // lane (lane tl < 4 holds Fp tl of a line: bx.x, bx.y, cy.x, cy.y), read from
@@ -770,6 +771,64 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
   ILfix::run(T, S, after);
 }
 
+// team_final_exp_fc (bn256_pairing.h) on layout S: the same chain over seven
+// slots F, A, B, C, D, E, G (the full layout spreads it over eleven), so the
+// team region is 120 elements instead of 180 and two pairing waves fit on a
+// SIMD's share of the LDS. Slot roles: F = res; the easy part's inversion
+// uses D, E; the exponentiations by v ping-pong D <-> E with the base's
+// conjugate in G; t0 = A, t1 = B, t2 = C, t4 = G, t3 = B (once t1 is
+// consumed); D carries the Frobenius temporaries of the last products.
+HG_DEV constexpr XHint final_exp_hint_s() { return xh<IMul12S<S_E, S_F, S_D>>(); }
+HG_DEV void team_final_exp_fc_s(const Team& T, XStream& S) {
+  // easy part: res = f^((p^6 - 1)(p^2 + 1)), f^-1 = conj(f) / (f conj(f))
+  t12_conj(T, S_D, S_F);
+  IMul12S<S_E, S_F, S_D>::run(T, S, xh<IMul12S<S_A, S_D, S_E>>());  // N = f conj(f)
+  t12_inv_norm(T, S_E);                                              // N^-1
+  IMul12S<S_A, S_D, S_E>::run(T, S, xh<IMul12S<S_F, S_B, S_A>>());  // A = f^-1
+  t12_conj(T, S_B, S_F);
+  IMul12S<S_F, S_B, S_A>::run(T, S, xh<IMul12S<S_F, S_F, S_A>>());  // f^(p^6 - 1)
+  t12_frob2(T, S_A, S_F);
+  IMul12S<S_F, S_F, S_A>::run(T, S, xh<ICycS<S_E, S_D>>());         // res
+  t12_copy(T, S_D, S_F);  // base of the first exponentiation
+#pragma unroll 1
+  for (int ph = 0; ph < 3; ph++) {
+#pragma unroll 1
+    for (int st = 0; st < 3; st++) {  // E = D^v, D = E^v, E = D^v
+      const XHint next = st < 2 ? ((st & 1) ? xh<ICycS<S_E, S_D>>() : xh<ICycS<S_D, S_E>>())
+                                : (ph == 0 ? xh<ICycS<S_A, S_A>>() : ph == 1 ? xh<IMul12S<S_B, S_C, S_G>>()
+                                                                             : xh<IMul12S<S_G, S_B, S_E>>());
+      if ((st & 1) == 0) t12_pow_v_s<S_E, S_D, S_G>(T, S, next);
+      else t12_pow_v_s<S_D, S_E, S_G>(T, S, next);
+    }
+    if (ph == 0) {  // t0 = conj(res^u)^2, t1 = t0^2 t0; next base t1
+      t12_conj(T, S_A, S_E);
+      ICycS<S_A, S_A>::run(T, S, xh<ICycS<S_B, S_A>>());
+      ICycS<S_B, S_A>::run(T, S, xh<IMul12S<S_B, S_A, S_B>>());
+      IMul12S<S_B, S_A, S_B>::run(T, S, xh<ICycS<S_E, S_D>>());
+      t12_copy(T, S_D, S_B);
+    } else if (ph == 1) {  // t2 = conj(t1^u), t1 = t2 conj(t1); next base t3 = t2^2
+      t12_conj(T, S_C, S_E);
+      t12_conj(T, S_G, S_B);
+      IMul12S<S_B, S_C, S_G>::run(T, S, xh<ICyc0S<S_D, S_C>>());
+      ICyc0S<S_D, S_C>::run(T, S, xh<ICycS<S_E, S_D>>());
+    } else {  // t4 = t1 t3^u
+      IMul12S<S_G, S_B, S_E>::run(T, S, xh<IMul12S<S_B, S_A, S_G>>());
+    }
+  }
+  IMul12S<S_B, S_A, S_G>::run(T, S, xh<IMul12S<S_A, S_C, S_G>>());  // t3 = t0 t4
+  IMul12S<S_A, S_C, S_G>::run(T, S, xh<IMul12S<S_A, S_F, S_A>>());  // t0 = t2 t4
+  IMul12S<S_A, S_F, S_A>::run(T, S, xh<IMul12S<S_A, S_D, S_A>>());  // t0 = res t0
+  t12_frob(T, S_D, S_B);
+  IMul12S<S_A, S_D, S_A>::run(T, S, xh<IMul12S<S_A, S_D, S_A>>());  // t0 = frob(t3) t0
+  t12_frob2(T, S_D, S_G);
+  IMul12S<S_A, S_D, S_A>::run(T, S, xh<IMul12S<S_D, S_D, S_B>>());  // t0 = frob2(t4) t0
+  t12_conj(T, S_D, S_F);
+  IMul12S<S_D, S_D, S_B>::run(T, S, xh<IMul12S<S_F, S_D, S_A>>());  // t2 = conj(res) t3
+  t12_frob(T, S_D, S_D);
+  t12_frob2(T, S_D, S_D);                                            // t2 = frob^3(t2)
+  IMul12S<S_F, S_D, S_A>::run(T, S, xh_none());                      // result
+}
+
 // true (team-uniform) when slots a and b hold the same value (both canonical)
 HG_DEV bool t12_equal(const Team& T, int a, int b) {
   Fp u, v;
@@ -784,11 +843,11 @@ HG_DEV bool t12_equal(const Team& T, int a, int b) {
 // FE(Miller(G2Base at -sig)) == Y_r  <=>  e(H, agg) * e(-sig, G2Base) == 1
 // kStore: write FE(Miller(G2Base at -sig)) to fe[r] instead (the fold runs
 // beside this kernel on a second stream; k_gt_compare finishes the check)
-// The team region ends after the last element the sig-only Miller loop and
-// the final exponentiation touch (kSigTeamElems, from the generator: slots F..L
-// and the FE pre-pass scratch, no pk-side G2 registers): 28.5 KB of LDS per
-// 4-team wave instead of k_verify's 33.9 KB, so four fold workgroups (9.6 KB
-// each) fit on a CU beside its four pairing waves.
+// The team region is layout S (kSigTeamElems, from the generator: slots F..G,
+// then the registers from kSigRegBase, the FE pre-pass scratch among them):
+// 19.2 KB of LDS per 4-team wave instead of k_verify's 33.9 KB, so the CU's
+// LDS holds its four pairing waves and the fold's workgroups beside them, or
+// eight pairing waves.
 static constexpr int kSigTeamWords = kSigTeamElems * 10;
 static_assert(kSigTeamWords % 2 == 0 && kSigTeamWords <= kTeamWords, "sig team region");
 // kStore: the signature is decoded here from its marshal (sig_bytes, the
@@ -796,7 +855,9 @@ static_assert(kSigTeamWords % 2 == 0 && kSigTeamWords <= kTeamWords, "sig team r
 // the side stream, off this kernel's critical path. A signature that fails to
 // decode gives a meaningless FE value, which k_gt_compare never reads (its code
 // is the decode error already).
-template <int TEAMS, bool kStore>
+// kPad: one pairing wave per SIMD (below); HG_SIG_PAD=0 launches the
+// unpadded variant, two waves per SIMD when two batches are in flight
+template <int TEAMS, bool kStore, bool kPad = (TEAMS == 4)>
 __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const uint8_t* sig_bytes, int flavor, int n,
                                                    const LineCoef* tab, const Gt* y, Gt* fe, int32_t* codes) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kSigTeamWords];
@@ -808,9 +869,9 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
   // second batch's pairing waves (two contexts in flight) share SIMDs and
   // crowd the fold's workgroups out of the CU's LDS; marking v255 and one
   // AGPR used makes its allocation exceed half of the 512-entry file
-  if constexpr (TEAMS == 4) asm volatile("" ::: "v255", "a0");
+  if constexpr (kPad) asm volatile("" ::: "v255", "a0");
   Team T = make_team(lds, kSigTeamWords);
-  uint32_t* F = team_regs(T);
+  uint32_t* F = T.base + kSigRegBase * 10;
   const int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
   const bool valid = idx < n;
   const int ci = valid ? idx : n - 1;
@@ -818,8 +879,8 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
   if (kStore) (void)decode_g1_one(sig_bytes + (size_t)ci * 64, flavor, sg);
   else sg = sigs[ci];
   XStream S = x_stream();
-  team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, final_exp_hint());
-  team_final_exp_fc(T, F, S);
+  team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, final_exp_hint_s());
+  team_final_exp_fc_s(T, S);
   if (kStore) {
     team_sync();
     if (valid) gt_store(T, S_F, fe + idx);
@@ -915,19 +976,25 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
   if (n > 0) k_verify_sig<4, false><<<nblk(n, 4), 64, 0, s>>>(sigs, nullptr, 0, n, tab, y, nullptr, codes);
 }
-// HG_SIG_TEAMS=2 (experiment): two checks per wave and no register padding,
-// so two pairing waves share each SIMD at a 4096 batch
-static int sig_teams() {
-  static const int t = [] {
-    const char* e = getenv("HG_SIG_TEAMS");
-    return e && atoi(e) == 2 ? 2 : 4;
+// Experiment knobs (A/B): HG_SIG_TEAMS=2 — two checks per wave, unpadded, so
+// two pairing waves share each SIMD at a 4096 batch; HG_SIG_PAD=0 — four
+// checks per wave, unpadded (two waves per SIMD once two batches overlap)
+static int sig_variant() {
+  static const int v = [] {
+    const char* t = getenv("HG_SIG_TEAMS");
+    if (t && atoi(t) == 2) return 2;
+    const char* p = getenv("HG_SIG_PAD");
+    return p && atoi(p) == 0 ? 1 : 0;
   }();
-  return t;
+  return v;
 }
 void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
   if (n <= 0) return;
-  if (sig_teams() == 2) k_verify_sig<2, true><<<nblk(n, 2), 32, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
-  else k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
+  switch (sig_variant()) {
+    case 2: k_verify_sig<2, true><<<nblk(n, 2), 32, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr); break;
+    case 1: k_verify_sig<4, true, false><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr); break;
+    default: k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
+  }
 }
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s) {
   if (n > 0) k_gt_compare<<<n, 64, 0, s>>>(fe, y, n, codes);

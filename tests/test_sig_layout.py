@@ -1,0 +1,164 @@
+"""k_verify_sig's final exponentiation on layout S (bn256_gt.hip
+team_final_exp_fc_s, bn256_xprog.h t12_pow_v_s): the chain runs over seven
+Fp12 slots, with several slots reused for different values along the way.
+
+This test reads the two device functions' text, turns their statements into
+operations on a slot dictionary (Fp12 values from the oracle) and runs them:
+the value left in slot F must be oracle.final_exponentiation_fc(f), so a slot
+overwritten while still needed shows up here, not only on the GPU. The team
+programs themselves (one table per call-site instance, layout S) are checked
+by tools/gen_g2_schedule.py check_instances (tests/test_g2_schedule.py).
+"""
+
+import os
+import random
+import re
+
+from oracle import bn256_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "handel_amd", "csrc")
+V = 1868033  # u = v^3 (bn256_xprog.h t12_pow_v_x)
+
+
+def _body(path, signature):
+    src = open(path).read()
+    i = src.index(signature)
+    i = src.index("{", i)
+    depth, j = 0, i
+    while True:
+        if src[j] == "{":
+            depth += 1
+        elif src[j] == "}":
+            depth -= 1
+            if depth == 0:
+                return src[i + 1:j]
+        j += 1
+
+
+def _to_python(body):
+    """The C++ subset these functions use -> Python source."""
+    body = re.sub(r"//[^\n]*", "", body)
+    body = re.sub(r"#pragma[^\n]*", "", body)
+    # drop the prefetch hints (declarations spanning lines up to ';')
+    body = re.sub(r"const XHint \w+ = [^;]*;", "", body, flags=re.S)
+    body = re.sub(r"static_assert\([^;]*;", "", body, flags=re.S)
+    body = re.sub(r"const int nsq\[4\] = \{([^}]*)\};", r"nsq = [\1]", body)
+    body = re.sub(r"const XHint mul = [^;]*;", "", body, flags=re.S)
+    out, depth = [], 0
+    for raw in body.replace("{", "{\n").replace("}", "\n}\n").split("\n"):
+        line = raw.strip()
+        if not line:
+            continue
+        if line == "}":
+            depth -= 1
+            continue
+        if line.startswith("} else"):
+            depth -= 1
+            line = line[1:].strip()
+
+        def stmt(s):
+            s = s.strip().rstrip(";")
+            m = re.match(r"t12_(conj|frob|frob2|copy)\(T, S_(\w), S_(\w)\)$", s)
+            if m:
+                return f"{m.group(1)}('{m.group(2)}', '{m.group(3)}')"
+            m = re.match(r"t12_inv_norm\(T, S_(\w)\)$", s)
+            if m:
+                return f"inv('{m.group(1)}')"
+            m = re.match(r"(IMul12S|IMul12)<S_(\w), S_(\w), S_(\w)>::run\(.*\)$", s)
+            if m:
+                return f"mul('{m.group(2)}', '{m.group(3)}', '{m.group(4)}')"
+            m = re.match(r"(ICycS|ICyc0S)<S_(\w), S_(\w)>::run\(.*\)$", s)
+            if m:
+                return f"sqr('{m.group(2)}', '{m.group(3)}')"
+            m = re.match(r"t12_pow_v_s<S_(\w), S_(\w), S_(\w)>\(.*\)$", s)
+            if m:
+                return f"powv('{m.group(1)}', '{m.group(2)}', '{m.group(3)}')"
+            m = re.match(r"(IMul12S|ICycS)<D, (\w+)(, (\w+))?>::run\(.*\)$", s)
+            if m:  # inside t12_pow_v_s: template slots D, SA, SK
+                return f"{'mul' if m.group(1) == 'IMul12S' else 'sqr'}(D, {m.group(2)}" + (
+                    f", {m.group(4)})" if m.group(4) else ")")
+            m = re.match(r"t12_conj\(T, (\w+), (\w+)\)$", s)
+            if m:
+                return f"conj({m.group(1)}, {m.group(2)})"
+            if s.startswith("nsq ="):
+                return s
+            raise ValueError(f"unhandled statement: {s!r}")
+
+        ind = "    " * depth
+        m = re.match(r"for \(int (\w+) = 0; \w+ < ([^;]+); \w+\+\+\) \{$", line)
+        if m:
+            out.append(f"{ind}for {m.group(1)} in range({m.group(2)}):")
+            depth += 1
+            continue
+        m = re.match(r"for \(int (\w+) = 0; \w+ < ([^;]+); \w+\+\+\) (.+;)$", line)
+        if m:
+            out.append(f"{ind}for {m.group(1)} in range({m.group(2)}):")
+            out.append(f"{ind}    {stmt(m.group(3))}")
+            continue
+        m = re.match(r"(else )?if \((.*)\) \{$", line)
+        if m:
+            cond = m.group(2).replace("&&", "and").replace("||", "or")
+            out.append(f"{ind}{'elif' if m.group(1) else 'if'} {cond}:")
+            depth += 1
+            continue
+        if line == "else {":
+            out.append(f"{ind}else:")
+            depth += 1
+            continue
+        m = re.match(r"if \(((?:[^()]|\([^()]*\))*)\) (.+;)$", line)
+        if m:
+            out.append(f"{ind}if {m.group(1)}:")
+            out.append(f"{ind}    {stmt(m.group(2))}")
+            continue
+        m = re.match(r"else (.+;)$", line)
+        if m:
+            out.append(f"{ind}else:")
+            out.append(f"{ind}    {stmt(m.group(1))}")
+            continue
+        out.append(ind + stmt(line))
+    return "\n".join(out)
+
+
+def test_final_exp_layout_s_matches_oracle():
+    fc_src = _to_python(_body(os.path.join(CSRC, "bn256_gt.hip"), "HG_DEV void team_final_exp_fc_s("))
+    pow_src = _to_python(_body(os.path.join(CSRC, "bn256_xprog.h"), "HG_DEV void t12_pow_v_s("))
+    rng = random.Random(5)
+    f = [(rng.randrange(O.P), rng.randrange(O.P)) for _ in range(6)]
+    slots = {}
+
+    def conj(d, a):
+        slots[d] = O.f12_conj(slots[a])
+
+    def frob(d, a):
+        slots[d] = O.f12_frob(slots[a])
+
+    def frob2(d, a):
+        slots[d] = O.f12_frob2(slots[a])
+
+    def copy(d, a):
+        slots[d] = slots[a]
+
+    def inv(d):
+        slots[d] = O.f12_inv(slots[d])
+
+    def mul(d, a, b):
+        slots[d] = O.f12_mul(slots[a], slots[b])
+
+    def sqr(d, a):
+        slots[d] = O.f12_sqr(slots[a])
+
+    env = {"conj": conj, "frob": frob, "frob2": frob2, "copy": copy, "inv": inv, "mul": mul, "sqr": sqr}
+
+    def powv(d, sa, sk):
+        assert len({d, sa, sk}) == 3
+        loc = dict(env, D=d, SA=sa, SK=sk)
+        exec(pow_src, loc)
+        assert slots[d] == O.f12_pow(slots[sa], V), "t12_pow_v_s"
+
+    env["powv"] = powv
+    for s in "FABCDEG":  # garbage everywhere but F
+        slots[s] = O.f12_pow(f, rng.randrange(2, 1000)) if s != "F" else f
+    exec(fc_src, dict(env))
+    assert set(slots) == set("FABCDEG"), "layout S uses slots F..G only"
+    assert slots["F"] == O.final_exponentiation_fc(f)

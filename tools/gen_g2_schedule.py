@@ -1161,11 +1161,35 @@ INSTANCES = sorted(set(
     + [("CYC_SQR_X", ("B", "A")), ("CYC_SQR", ("I", "C"))]
     + [("MUL12", b) for b in [("B", "A", "B"), ("B", "C", "D"), ("E", "B", "J"), ("D", "A", "E"), ("A", "C", "E"),
                               ("A", "F", "A"), ("A", "G", "A"), ("G", "G", "D"), ("F", "G", "A")]]
-    # bn256_gt.hip: the sig-only Miller loop and the GT fold
-    + [("SDBL", ("F", "F")), ("LFEV", ("F", "F")), ("FEVAL", ()), ("MUL12F", ("A", "A", "B"))]))
+    # bn256_gt.hip: the GT fold
+    + [("MUL12F", ("A", "A", "B"))]))
+
+# k_verify_sig's compact team region (layout "S", bn256_gt.hip): slots F, A, B,
+# C, D, E, G — the sig-only Miller loop and the Fuentes-Castaneda final
+# exponentiation (team_final_exp_fc_s) need no more — then the register file.
+# The Miller loop's pre-pass scratch lies in slots A.. (only F is live there),
+# the final exponentiation's past register ONE (the Miller registers are dead
+# there), as in the full layout. 120 elements per team instead of 180: 19.2 KB
+# of LDS per 4-team wave, so two pairing waves fit on a SIMD.
+SIG_SLOTS = SLOTS[:7]
+SIG_F_BASE = 12 * len(SIG_SLOTS)
+SIG_SCR_BASE = {"FE": SIG_F_BASE + 2, "ML": 12 * SLOTS.index("A")}
+SIG_INSTANCES = sorted(set(
+    [("SDBL", ("F", "F")), ("LFEV", ("F", "F")), ("FEVAL", ()), ("LINE_FIX", ("F", "F"))]
+    # the easy part (inversion scratch D, E) and the exponentiations by v
+    # (D <-> E, conjugate of the base in G)
+    + [("MUL12", b) for b in [("E", "F", "D"), ("A", "D", "E"), ("F", "B", "A"), ("F", "F", "A"),
+                              ("E", "E", "G"), ("E", "E", "D"), ("D", "D", "G"), ("D", "D", "E"),
+                              ("B", "A", "B"), ("B", "C", "G"), ("G", "B", "E"), ("B", "A", "G"),
+                              ("A", "C", "G"), ("A", "F", "A"), ("A", "D", "A"), ("D", "D", "B"), ("F", "D", "A")]]
+    + [("CYC_SQR_X", b) for b in [("E", "D"), ("E", "E"), ("D", "E"), ("D", "D"), ("A", "A"), ("B", "A")]]
+    + [("CYC_SQR", ("D", "C"))]))
+ALL_INSTANCES = [(n, b, "") for n, b in INSTANCES] + [(n, b, "S") for n, b in SIG_INSTANCES]
 
 
-def bind(xr, binding, ctx):
+
+
+def bind(xr, binding, ctx, layout=""):
     """Translates a compiled round to absolute team element indices."""
     D, A, B = (list(binding) + [None, None, None])[:3]
     if len(binding) == 2:
@@ -1173,6 +1197,10 @@ def bind(xr, binding, ctx):
         B = A
     sbase = SCR_BASE[ctx]
     fbase = F_BASE_CTX[ctx]
+    region_end = REGION_END[ctx]
+    if layout == "S":
+        assert ctx in SIG_SCR_BASE and all(b in SIG_SLOTS for b in binding), "layout S: slots F..G only"
+        sbase, fbase, region_end = SIG_SCR_BASE[ctx], SIG_F_BASE, SIG_F_BASE + NREGS_RUNTIME
 
     def src(code):
         if code >= X_SCR:
@@ -1206,7 +1234,9 @@ def bind(xr, binding, ctx):
         srcs = [u for u, v in L["prod"] + L.get("prod2", [])] + [v for u, v in L["prod"] + L.get("prod2", [])]
         srcs += [s_ for s_, _ in L["lin"] + L.get("lin2", [])] + [s_ for _, t in L["pre"] for s_, _ in t]
         for v in [L["dst"], L.get("dst2", NONE)] + [d for d, _ in L["pre"]] + srcs:
-            assert v == NONE or v < REGION_END[ctx], "index out of the kernels' team region"
+            assert v == NONE or v < region_end, "index out of the kernels' team region"
+        if layout == "S" and ctx == "ML":  # the Miller scratch stays inside slots A..G
+            assert all(d == NONE or 12 <= d < SIG_F_BASE for d, _ in L["pre"]), "layout S: ML scratch"
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
     out.ks1, out.ks2 = xr.ks1, xr.ks2
@@ -1234,10 +1264,10 @@ def run_bound(rounds, mem):
 def check_instances(X, seed=3):
     """Every bound instance computes the same as the abstract program."""
     rng = random.Random(seed)
-    for name, binding in INSTANCES:
+    for name, binding, layout in ALL_INSTANCES:
         ctx = X_PROGRAMS[name]
-        fb = F_BASE_CTX[ctx]
-        rounds = [bind(xr, binding, ctx) for xr in X[name]]
+        fb = SIG_F_BASE if layout == "S" else F_BASE_CTX[ctx]
+        rounds = [bind(xr, binding, ctx, layout) for xr in X[name]]
         mem = [rng.randrange(P) for _ in range(F_BASE + NREGS)]
         mem[fb + REG["ZERO"]] = 0
         mem[fb + REG["ONE"]] = 1
@@ -1276,34 +1306,36 @@ def touched(bx):
 
 
 def emit_x(X, path):
-    sig_end = F_BASE + REG["FC.y"] + 1  # team_miller_sig's registers: ZERO .. FC
-    fold_end = FOLD_F_BASE + 2           # ZERO, ONE
-    for name, binding in INSTANCES:
+    sig_end = SIG_F_BASE + REG["FC.y"] + 1  # team_miller_sig's registers: ZERO .. FC
+    fold_end = FOLD_F_BASE + 2               # ZERO, ONE
+    for name, binding, layout in ALL_INSTANCES:
         ctx = X_PROGRAMS[name]
         for xr in X[name]:
-            t = touched(bind(xr, binding, ctx)) + 1
-            if name in SIG_PROGRAMS and ctx in ("FE", "ML"):
+            t = touched(bind(xr, binding, ctx, layout)) + 1
+            if layout == "S":
                 sig_end = max(sig_end, t)
             if ctx == "FOLD":
                 fold_end = max(fold_end, t)
+    sig_names = sorted({n for n, _, lay in ALL_INSTANCES if lay == "S"}, key=list(X_PROGRAMS).index)
     lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
              "// Two-phase team programs executed by bn256_xprog.h (encoding: see there),",
              "// one table per call-site instance (absolute team element indices).",
              "#pragma once", "#include <stdint.h>", "namespace hg {",
              f"// HG_P2N: ({NEG_MULT}p)'' (the negation constant of pre-pass and linear terms)",
              "#define HG_P2N " + ", ".join("0x%08xu" % v for v in P2N),
-             "enum XProg { " + ", ".join(f"XP_{n}" for n in X_PROGRAMS) + " };",
+             "enum XProg { " + ", ".join([f"XP_{n}" for n in X_PROGRAMS] + [f"XP_{n}_S" for n in sig_names]) + " };",
              f"static constexpr int kXFetchWords = {X_FETCH_WORDS};",
              f"static constexpr int kFoldRegBase = {FOLD_F_BASE};  // FOLD team region: ZERO, ONE here",
              f"static constexpr int kFoldTeamElems = {fold_end + fold_end % 2};  // elements the fold programs touch",
-             f"static constexpr int kSigTeamElems = {sig_end + sig_end % 2};  // k_verify_sig's team region",
+             f"static constexpr int kSigRegBase = {SIG_F_BASE};  // k_verify_sig's layout S: registers here",
+             f"static constexpr int kSigTeamElems = {sig_end + sig_end % 2};  // k_verify_sig's team region (layout S)",
              "template <int PROG, int D = -1, int A = -1, int B = -1> struct XInst;"]
     words = []
-    for name, binding in INSTANCES:
+    for name, binding, layout in ALL_INSTANCES:
         ctx = X_PROGRAMS[name]
         rounds = []
         for xr in X[name]:
-            bx = bind(xr, binding, ctx)
+            bx = bind(xr, binding, ctx, layout)
             off = len(words)
             for t in range(16):
                 hv = bx.lane_halves(t)
@@ -1325,7 +1357,7 @@ def emit_x(X, path):
             calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
                          f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}, {bx.ef}, {fu}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
-        targs = f"XP_{name}" + (", " + args if args else "")
+        targs = f"XP_{name}{'_S' if layout == 'S' else ''}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
                      f"kW = {rounds[0][0].words()}; HG_DEV static void run(const Team& T, XStream& S, XHint h) {{ "
                      + " ".join(calls) + " } };")
@@ -1406,7 +1438,7 @@ if __name__ == "__main__":
     Xp = validate_x()
     check_instances(Xp)
     nwords = emit_x(Xp, os.path.join(csrc, "bn256_xtab.h"))
-    print(len(INSTANCES), "instances,", nwords * 4, "table bytes")
+    print(len(ALL_INSTANCES), "instances,", nwords * 4, "table bytes")
     for name, rounds in Xp.items():
         print(name, [(r.nv, r.nt, r.np, r.nl, r.words()) for r in rounds])
     print("validated and wrote bn256_g2sched.h, bn256_xtab.h")
