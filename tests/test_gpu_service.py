@@ -141,7 +141,7 @@ def test_verifierd_serves_registry_file(tmp_path, reg300):
         ready = json.loads(p.stdout.readline() or "{}")
         assert ready.get("ready") == name and ready["registry"] == NREG and ready["tables"] == 2, p.stderr.read()
         with Client(name) as cl:
-            assert cl.flavor() == 0
+            assert cl.flavor == 0
             got = cl.verify_many(F.LIB_MESSAGE, reqs, words, sigs)
         assert np.array_equal(got, want)
     finally:
