@@ -49,8 +49,8 @@ struct GtWork {
   int win_bits;    // 8 or 16: which window table `win` is
 };
 
-// the 6-lane Karatsuba fold and 16-key table kernels (bn256_k6.h); HG_GT_K6=0
-// selects the 12-lane team programs instead (A/B runs)
+// the 6-lane Karatsuba fold and 16-key table kernels (bn256_k6.h) with
+// HG_GT_K6=1; the 12-lane team programs otherwise (the default: faster)
 bool gt_k6();
 // G_i = e(H, pk_i) for the n registry keys
 void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s);

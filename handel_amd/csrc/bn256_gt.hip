@@ -269,10 +269,12 @@ __global__ __launch_bounds__(64, 2) void k_gt_win16_6(const Gt* w8, int nwin8, i
   }
 }
 
+// The 6-lane fold is opt-in (HG_GT_K6=1): measured slower than the 12-lane
+// kernels (profiles/r04_k6_ab.json)
 bool gt_k6() {
   static const bool on = [] {
     const char* e = getenv("HG_GT_K6");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

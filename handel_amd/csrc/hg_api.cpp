@@ -795,7 +795,7 @@ static int ensure_gt_fold(hg_ctx* c, Ws& ws, size_t n, const FoldCaps& caps, GtW
   w.cap = (int)caps.chunks;
   w.multi = ws.gt_multi.p;
   w.partial = ws.gt_partial.p;
-  // the 6-lane Karatsuba fold (bn256_k6.h) unless HG_GT_K6=0 (A/B runs)
+  // the 6-lane Karatsuba fold (bn256_k6.h) with HG_GT_K6=1 (opt-in: measured slower)
   const int k6 = gt_k6() ? 1 : 0;
   w.k6 = k6;
   const size_t per_wg = k6 ? 10 : kGtChunkTeams;
