@@ -182,6 +182,10 @@ struct hg_service {
   int built_level = 0;
   uint64_t max_in_flight = 0;
   Clock::time_point last_arrival;
+  // requests released by finished batches whose clients have not submitted
+  // again (cfg.follow): a closed-loop cohort is back when this reaches zero
+  uint64_t returning = 0;
+  bool released_any = false;
   std::vector<uint32_t> take;
 
   bool intake();
@@ -208,6 +212,7 @@ bool hg_service::intake() {
       if (s->state.load(std::memory_order_acquire) != kSlotQueued) continue;
       s->state.store(kSlotTaken, std::memory_order_relaxed);
       pending.push_back(Pending{id, s->msg, s->msg_gen, now});
+      if (returning) returning--;
       any = true;
     }
   }
@@ -241,6 +246,8 @@ void hg_service::finish_slots(const uint32_t* ids, size_t n, const int32_t* code
 void hg_service::complete(int lane, const int32_t* codes, int32_t fail) {
   LaneState& L = lanes[lane];
   finish_slots(L.slots.data(), L.slots.size(), codes, fail);
+  returning += L.slots.size();
+  released_any = true;
   v.h->batches.fetch_add(1, std::memory_order_relaxed);
   v.h->requests.fetch_add(L.slots.size(), std::memory_order_relaxed);
   L.slots.clear();
@@ -380,7 +387,9 @@ void hg_service::run() {
       const bool old = now - pending.front().seen >= linger;
       // a burst of resubmissions (the clients of a finished batch) has ended
       const bool calm = cfg.quiet_us && now - last_arrival >= quiet;
-      if (!full && !old && !calm && !stopping) break;
+      // every request the finished batches released has been submitted again
+      const bool back = cfg.follow && released_any && returning == 0;
+      if (!full && !old && !calm && !back && !stopping) break;
       launch(free_lane);
       progress = true;
     }
@@ -482,6 +491,7 @@ void hg_service_config_init(hg_service_config* c) {
   c->max_batch = 4096;
   c->max_wait_us = 50;
   c->quiet_us = 0;
+  c->follow = 1;
   c->prepare = 1;
   c->overlap = 1;
 }

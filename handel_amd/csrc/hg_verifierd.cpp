@@ -8,7 +8,7 @@
 //
 //   hg_verifierd --name /handel --registry reg.bin [--flavor go|cf] [--device 0]
 //                [--message msg.bin] [--lanes 8] [--max-batch 4096]
-//                [--max-wait-us 50] [--quiet-us 0] [--policy] [--overlap 1]
+//                [--max-wait-us 50] [--quiet-us 0] [--follow 1] [--policy] [--overlap 1]
 //   hg_verifierd --name /handel --echo US --nreg N      (CPU stand-in, no GPU)
 //
 // reg.bin: n x 128-byte marshalled public keys in registry order
@@ -44,7 +44,7 @@ int usage() {
   fprintf(stderr,
           "usage: hg_verifierd --name /NAME (--registry FILE | --echo US --nreg N) [--flavor go|cf] [--device D]\n"
           "                    [--message FILE] [--lanes L] [--max-batch B] [--max-wait-us U] [--quiet-us Q]\n"
-          "                    [--policy] [--overlap 0|1] [--slots S]\n");
+          "                    [--follow 0|1] [--policy] [--overlap 0|1] [--slots S]\n");
   return 2;
 }
 
@@ -79,6 +79,7 @@ int main(int argc, char** argv) {
     else if (a == "--quiet-us") cfg.quiet_us = (uint32_t)atoi(need());
     else if (a == "--slots") cfg.slots = (uint32_t)atoi(need());
     else if (a == "--overlap") cfg.overlap = atoi(need());
+    else if (a == "--follow") cfg.follow = atoi(need());
     else if (a == "--policy") cfg.prepare = 0;
     else if (a == "--echo") echo_us = atol(need());
     else if (a == "--nreg") nreg_echo = atol(need());

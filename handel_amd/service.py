@@ -30,7 +30,7 @@ class ServiceConfig(ctypes.Structure):
     _fields_ = [("slots", ctypes.c_uint32), ("slot_bits", ctypes.c_uint32), ("channels", ctypes.c_uint32),
                 ("lanes", ctypes.c_uint32), ("max_batch", ctypes.c_uint32), ("max_wait_us", ctypes.c_uint32),
                 ("quiet_us", ctypes.c_uint32),
-                ("prepare", ctypes.c_int32), ("overlap", ctypes.c_int32)]
+                ("prepare", ctypes.c_int32), ("overlap", ctypes.c_int32), ("follow", ctypes.c_int32)]
 
 
 def _config(L, **kw) -> ServiceConfig:

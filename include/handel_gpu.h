@@ -407,6 +407,9 @@ typedef struct {
   int32_t prepare;      /* 1 (default): a message's first batch builds its top GT table level;
                            0: the context's volume policy (levels 1 and 2 after 16384 / 2^20 requests) */
   int32_t overlap;      /* 1 (default): the GT fold beside the pairing kernel inside each lane */
+  int32_t follow;       /* 1 (default): ... or as soon as as many requests have arrived as finished
+                           batches released (clients that submit their next check on a verdict:
+                           the whole cohort is back), whichever comes first; 0: off */
 } hg_service_config;
 void hg_service_config_init(hg_service_config* cfg);
 /* Creates the region (fails if `name` exists) and starts the dispatcher. */

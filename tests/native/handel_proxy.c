@@ -43,6 +43,7 @@
  *   -Q q   daemon: GPU_MAX_HW_QUEUES of the server (default 2 x lanes: a lane's two streams
  *          each on a hardware queue of their own)
  *   -q us  daemon: launch once no request has arrived for us microseconds (0: off)
+ *   -F 0|1 daemon: launch once every request the finished batches released is back (1)
  *   -E us  daemon: serve with the CPU echo stand-in (no GPU; protocol test),
  *          each batch taking `us` microseconds
  *   -C lib daemon: libhandel_client.so (default: next to libhandel_gpu.so)
@@ -225,6 +226,7 @@ static int range_level(uint32_t id, uint32_t size, int level, uint32_t* lo, uint
 typedef struct {
   int procs, inst, nreg, checks, workers, max_batch, wait_us, prepare, level, daemon, lanes, overlap, queues, quiet_us;
   long budget_mb, echo_us;
+  int follow;
   const char* dump;
   const char* lib;
   const char* client_lib;
@@ -506,6 +508,7 @@ static void run_server(const opts* o, pid_t parent, int ready_fd, int stop_fd, i
   cfg.max_batch = (uint32_t)o->max_batch;
   cfg.max_wait_us = (uint32_t)o->wait_us;
   cfg.quiet_us = (uint32_t)o->quiet_us;
+  cfg.follow = o->follow;
   cfg.prepare = o->prepare;
   cfg.overlap = o->overlap;
   cfg.slot_bits = (uint32_t)o->nreg;
@@ -704,11 +707,12 @@ static int dump_process0(const opts* o) {
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <libhandel_gpu.so> [-p P] [-k K] [-n N] [-r R] [-w W] [-b B] [-u U] [-P 0|1] "
-                    "[-L level] [-M MB] [-D 0|1] [-l lanes] [-o 0|1] [-Q queues] [-E us] [-C client.so] [-d DIR]\n",
+                    "[-L level] [-M MB] [-D 0|1] [-l lanes] [-o 0|1] [-Q queues] [-q us] [-F 0|1] [-E us] [-C client.so] "
+                    "[-d DIR]\n",
             argv[0]);
     return 2;
   }
-  opts o = {8, 250, 2000, 45, -1, 4096, -1, 0, -1, 0, 8, 1, 0, 0, -1, -1, NULL, argv[1], NULL};
+  opts o = {8, 250, 2000, 45, -1, 4096, -1, 0, -1, 0, 8, 1, 0, 0, -1, -1, 1, NULL, argv[1], NULL};
   for (int i = 2; i + 1 < argc; i += 2) {
     const char* f = argv[i];
     const char* v = argv[i + 1];
@@ -727,6 +731,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(f, "-o")) o.overlap = atoi(v);
     else if (!strcmp(f, "-Q")) o.queues = atoi(v);
     else if (!strcmp(f, "-q")) o.quiet_us = atoi(v);
+    else if (!strcmp(f, "-F")) o.follow = atoi(v);
     else if (!strcmp(f, "-E")) o.echo_us = atol(v);
     else if (!strcmp(f, "-C")) o.client_lib = v;
     else if (!strcmp(f, "-d")) o.dump = v;
@@ -860,14 +865,14 @@ int main(int argc, char** argv) {
   printf("{\"harness\": \"handel_proxy\", \"what\": \"config-4 process-model proxy (not Handel completion time)\", "
          "\"model\": \"%s\", \"procs\": %d, \"instances_per_proc\": %d, \"nodes\": %d, \"registry\": %d, "
          "\"checks_per_instance\": %d, \"workers_per_proc\": %d, \"prepare\": %d, \"lanes\": %d, \"overlap\": %d, "
-         "\"hw_queues\": %d, \"max_wait_us\": %d, \"quiet_us\": %d, \"echo_us\": %ld, \"tables_before\": %d, \"tables_after\": %d, "
+         "\"hw_queues\": %d, \"max_wait_us\": %d, \"quiet_us\": %d, \"follow\": %d, \"echo_us\": %ld, \"tables_before\": %d, \"tables_after\": %d, "
          "\"requests\": %llu, \"batches\": %llu, \"mean_batch\": %.1f, \"max_batches_in_flight\": %llu, "
          "\"wall_ms\": %.3f, \"throughput\": %.1f, "
          "\"latency_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
          "\"hbm_per_context_bytes\": %llu, \"hbm_total_bytes\": %llu, \"contexts\": %d, "
          "\"setup_s_max\": %.3f, \"prepare_ms_max\": %.3f, \"mismatches\": %llu}\n",
          o.daemon ? (o.echo_us >= 0 ? "daemon-echo" : "daemon") : "contexts", o.procs, o.inst, o.procs * o.inst,
-         o.nreg, o.checks, o.workers, o.prepare, o.daemon ? o.lanes : 1, o.overlap, o.queues, o.wait_us, o.quiet_us, o.echo_us,
+         o.nreg, o.checks, o.workers, o.prepare, o.daemon ? o.lanes : 1, o.overlap, o.queues, o.wait_us, o.quiet_us, o.follow, o.echo_us,
          tb, ta, (unsigned long long)reqs, (unsigned long long)batches, batches ? (double)reqs / batches : 0.0,
          (unsigned long long)in_flight, wall * 1e3, wall > 0 ? reqs / wall : 0.0, 1e6 * lat[m / 2],
          1e6 * lat[(m * 9) / 10], 1e6 * lat[(m * 99) / 100], 1e6 * lat[m - 1], (unsigned long long)bytes_max,
