@@ -10,14 +10,21 @@ Requests are a random node's random Handel level (partitioner rangeLevel), a
 bitset of density U[0.5, 1], the aggregate signature of the set bits, 1/8 of
 the aggregates tampered. Inputs (requests, bitset words, signatures) are
 resident in HBM; verdict codes are written to HBM, packed into a bitset and
-all-gathered over RCCL (the only cross-GPU traffic).
+all-gathered over RCCL (the only cross-GPU traffic). The verifier serves a
+continuous stream of such batches: two are in flight at a time on the
+context's lanes (hg_lane_submit_device: own streams and workspaces over the
+one registry and table set, the unpadded pairing kernel), so one batch's
+pairing waves share the SIMDs with the next one's (--inflight 1: one batch at
+a time, the `sequential` sub-line).
 
 Sub-lines (never `value`):
+  sequential      the headline batch one at a time on the context's stream
   single          config 2: 4096 independent single-signature checks
                   (simul/p2p/aggregator.go:244 verifyPacket)
   full_registry   config 3's VerifyMultiSignature shape: every request spans
                   the whole registry (crypto.go:120-137)
-  pipelined       two headline batches in flight on two HIP streams
+  pipelined       two headline batches in flight on two engine contexts
+                  (each with its own tables; the r03 form of the headline)
 --committees switches the headline to config 5: each rank is one committee of
 4096 signers (its own 4096-key registry) verifying 4096 multisignatures.
 
@@ -44,7 +51,7 @@ import torch  # noqa: E402
 
 from handel_amd import _lib  # noqa: E402
 from handel_amd.distributed import gather_verdicts, pack_verdicts  # noqa: E402
-from handel_amd.engine import REQ_DTYPE, Engine  # noqa: E402
+from handel_amd.engine import REQ_DTYPE, DeviceLane, Engine  # noqa: E402
 
 LIB_MESSAGE = b"Everything that is beautiful and noble is the product of reason and calculation."
 ORDER = 65000549695646603732796438742359905742570406053903786389881062969044166799969
@@ -711,6 +718,9 @@ def main():
                     help="config 5: each rank is one committee of 4096 signers (own 4096-key registry)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="headline only (no single / full / pipelined lines)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="headline: batches in flight on the context's lanes (1: one batch at a time on the "
+                         "context's stream)")
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight for the 'pipelined' line (1: skip)")
     ap.add_argument("--pipeline-overlap", type=int, default=1,
                     help="the pipelined line's contexts run their fold beside the pairing kernel (1) or before it (0)")
@@ -752,28 +762,70 @@ def main():
     head = AggregateWorkload(eng, n_reg, n, seed=4321 + rank, dev=dev, stream=stream)
     gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev) for _ in range(world)]
 
-    def step():
-        # the batch's verdicts and their bitset (bit i = check i valid), then
-        # the bitsets gathered over RCCL: the only cross-GPU traffic
+    def seq_step():
+        # one batch at a time on the context's stream: the batch's verdicts and
+        # their bitset (bit i = check i valid), then the bitsets gathered over
+        # RCCL: the only cross-GPU traffic
         head.submit_bits()
         gather_verdicts(head.d_bits.to(coll_dev), world, gathered)
 
-    step()
+    # the headline: a verifier fed a continuous stream of 4096-request batches
+    # keeps `inflight` of them in flight on the context's lanes (hg_lane_*:
+    # own streams and workspaces, the one registry and table set, the unpadded
+    # pairing kernel so two batches' waves share the SIMDs); each step is one
+    # whole batch — its verdicts, bitset and gather — on the lane's stream
+    inflight = max(1, args.inflight)
+    lanes, lane_out = [], []
+    if inflight > 1:
+        for i in range(inflight):
+            lanes.append(DeviceLane(eng, n, pad=False))
+            codes_i = head.d_codes if i == 0 else torch.zeros(n, dtype=torch.int32, device=dev)
+            bits_i = head.d_bits if i == 0 else torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
+            gath_i = gathered if i == 0 else [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev)
+                                              for _ in range(world)]
+            lane_out.append((torch.cuda.Stream(dev), codes_i, bits_i, gath_i))
+    turn = [0]
+
+    def lane_step():
+        i = turn[0] % inflight
+        turn[0] += 1
+        st, codes_i, bits_i, gath_i = lane_out[i]
+        with torch.cuda.stream(st):
+            lanes[i].submit_device(head.d_reqs.data_ptr(), n, head.d_words.data_ptr(), head.d_sigs.data_ptr(),
+                                   codes_i.data_ptr(), bits_i.data_ptr(), st.cuda_stream)
+            gather_verdicts(bits_i.to(coll_dev), world, gath_i)
+
+    step = lane_step if inflight > 1 else seq_step
+    for _ in range(inflight):
+        step()
     torch.cuda.synchronize(dev)
-    head.check()
+    for codes_i in ([o[1] for o in lane_out] if lanes else [head.d_codes]):
+        head.check(codes_i)
     assert torch.equal(head.d_bits, pack_verdicts(head.d_codes)), "HIP verdict bitset differs from the codes"
     prewarm_steps = timer.prewarm(step, args.prewarm)
     dt = timer.run(step, args.steps, args.warmup)
     rank_ms = [round(t / args.steps * 1e3, 4) for t in timer.rank_times]
-    head.check()
-    # every rank's gathered bitset: each rank tampers every 8th aggregate of
+    # every rank's gathered bitsets: each rank tampers every 8th aggregate of
     # its own batch, so all world bitsets equal this rank's expected one
     want = pack_verdicts(torch.from_numpy(head.expect))
     gather_check = {"world_size_seen": tdist.get_world_size() if dist else 1, "backend": backend if dist else None,
-                    "ranks_checked": world}
-    for r in range(world):
-        g = gathered[r] if dist else head.d_bits
-        assert torch.equal(g.cpu(), want), f"gathered bitset of rank {r} differs"
+                    "ranks_checked": world, "lanes_checked": max(1, len(lanes))}
+    for codes_i, bits_i, gath_i in ([(o[1], o[2], o[3]) for o in lane_out] if lanes
+                                    else [(head.d_codes, head.d_bits, gathered)]):
+        head.check(codes_i)
+        for r in range(world):
+            g = gath_i[r] if dist else bits_i
+            assert torch.equal(g.cpu(), want), f"gathered bitset of rank {r} differs"
+    for ln in lanes:
+        ln.close()
+    sequential = None
+    if inflight > 1 and not args.no_extra:
+        sdt_seq = timer.run(seq_step, args.steps, args.warmup)
+        head.check()
+        sequential = {"value": round(n * args.steps * world / sdt_seq, 1), "unit": "verifications/s",
+                      "ms_per_step": round(sdt_seq / args.steps * 1e3, 4),
+                      "what": "the headline batch one at a time on the context's stream (the next batch starts "
+                              "after the previous one's verdicts): the latency-bound rate, padded pairing kernel"}
     ph = timed_phases(eng, lambda: [head.submit() for _ in range(5)])
     # the kernels on their own (fold, then the pairing kernel: no overlap),
     # for the per-kernel rooflines
@@ -789,11 +841,11 @@ def main():
     impl_fpmul = head.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING
     roof = roofline(impl_fpmul, agg_ms, "the GT submission: k_agg_prologue, k_verify_sig beside the GT fold "
                     "(k_gt_plan, k_gt_chunks, k_gt_combine), k_gt_compare_bits",
-                    r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare_bits)|k_verify_sig<4, true>",
+                    r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare_bits)|k_verify_sig<4, true(, (true|false))?>",
                     f"implemented work: {head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 "
                     f"product each) + {n} x {FPMUL_PER_SIG_PAIRING} Fp-mul (one pairing + final exponentiation "
                     f"per check), x {MADS_PER_FPMUL} u32 mads",
-                    rocprof_pattern=r"k_verify_sig<4, true>|k_gt_compare_bits")
+                    rocprof_pattern=r"k_verify_sig<4, true(, (true|false))?>|k_gt_compare_bits")
     roof["frac_rocprof_note"] = ("the same work over the rocprof averages of the step's critical path (the pairing "
                                  "kernel, then the comparison; the fold runs beside it) in the driver-invocation "
                                  "profile")
@@ -807,10 +859,10 @@ def main():
                          f"(G2 addition) + {FPMUL_REFERENCE_CHECK} (two-pairing check), x {MADS_PER_FPMUL} u32 mads; mean "
                          f"{head.signers.mean():.1f} set bits",
                  "note": "work the GT path does not run is credited here; not a fraction of any peak"}
-    roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph_seq["verify"], "k_verify_sig", r"k_verify_sig<4, false>",
+    roof_verify = roofline(n * FPMUL_PER_SIG_PAIRING, ph_seq["verify"], "k_verify_sig", r"k_verify_sig<4, false(, true)?>",
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
                            "+ final exponentiation, oracle op count); kernel alone (fold not beside it)",
-                           rocprof_pattern=r"k_verify_sig<4, true>")
+                           rocprof_pattern=r"k_verify_sig<4, true(, (true|false))?>")
     roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph_seq["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
                          r"k_gt_(plan<16>|chunks|combine)",
                          f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each); "
@@ -885,7 +937,7 @@ def main():
             "kernels_ms": {k: round(v, 4) for k, v in fph.items() if v is not None},
             "roofline": roofline(full.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING, fph["submit"],
                                  "the GT submission (as the headline)",
-                                 r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare(?!_))|k_verify_sig<4, true>",
+                                 r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare(?!_))|k_verify_sig<4, true(, (true|false))?>",
                                  f"implemented work: {full.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul + "
                                  f"{n} x {FPMUL_PER_SIG_PAIRING} Fp-mul, x {MADS_PER_FPMUL} u32 mads")}
         del full
@@ -950,6 +1002,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "batches_in_flight": inflight,
             "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
             "prewarm": {"seconds": args.prewarm, "steps": prewarm_steps, "what": "untimed headline steps before the "
                         "warmup steps (GPU clocks settled whatever the warmup count)"},
@@ -964,7 +1017,8 @@ def main():
                        "batch_per_gpu": n, "registry": n_reg, "message": "lib.Message (81 B)",
                        "signers_per_check_mean": round(float(head.signers.mean()), 1),
                        "signers_per_check_max": int(head.signers.max()),
-                       "parallelism": f"dp{world} (one batch per GPU, RCCL all_gather of verdict bitsets)"},
+                       "parallelism": f"dp{world} (batches per GPU, {inflight} in flight on the context's lanes; RCCL "
+                                      "all_gather of verdict bitsets)"},
             "roofline": roof,
             "effective_rate": effective,
             "roofline_k_verify": roof_verify,
@@ -975,6 +1029,7 @@ def main():
                       "cold_value": round(n / ((head.setup_ms + dt / args.steps * 1e3) * 1e-3), 1)},
             "cpu_baseline": cpu,
             "gpu_over_cpu": (round(value / cpu["value"], 1) if cpu and cpu.get("value") else None),
+            "sequential": sequential,
             **extra,
         }
         print(json.dumps(line))

@@ -71,7 +71,8 @@ void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt
 // the same check in two launches, so the fold can run beside the pairing:
 // fe[r] = FE(Miller(G2Base at -sig_r)) from the 64-byte marshals (decoded in
 // the kernel), then fe[r] == y[r] where still HG_OK
-void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s);
+void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s,
+                        bool pad = true);
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s);
 // the same, and the verdict bitset (ceil(n / 8) bytes, hg_pack_verdicts_device's layout)
 void launch_gt_compare_bits(const Gt* fe, const Gt* y, int n, int32_t* codes, uint8_t* bits, hipStream_t s);

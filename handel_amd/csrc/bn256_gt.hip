@@ -978,25 +978,31 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
   if (n > 0) k_verify_sig<4, false><<<nblk(n, 4), 64, 0, s>>>(sigs, nullptr, 0, n, tab, y, nullptr, codes);
 }
-// Experiment knobs (A/B): HG_SIG_TEAMS=2 — two checks per wave, unpadded, so
-// two pairing waves share each SIMD at a 4096 batch; HG_SIG_PAD=0 — four
-// checks per wave, unpadded (two waves per SIMD once two batches overlap)
-static int sig_variant() {
+// pad (the default): one pairing wave per SIMD (k_verify_sig above); lanes
+// that keep two batches in flight launch the unpadded variant, so the second
+// batch's waves share the SIMDs. Experiment knobs (A/B): HG_SIG_TEAMS=2 — two
+// checks per wave, unpadded; HG_SIG_PAD=0/1 — overrides `pad`.
+static int sig_env() {
   static const int v = [] {
     const char* t = getenv("HG_SIG_TEAMS");
     if (t && atoi(t) == 2) return 2;
     const char* p = getenv("HG_SIG_PAD");
-    return p && atoi(p) == 0 ? 1 : 0;
+    if (!p) return -1;
+    return atoi(p) == 0 ? 0 : 1;
   }();
   return v;
 }
-void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
+void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s,
+                        bool pad) {
   if (n <= 0) return;
-  switch (sig_variant()) {
-    case 2: k_verify_sig<2, true><<<nblk(n, 2), 32, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr); break;
-    case 1: k_verify_sig<4, true, false><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr); break;
-    default: k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
+  const int env = sig_env();
+  if (env == 2) {
+    k_verify_sig<2, true><<<nblk(n, 2), 32, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
+    return;
   }
+  if (env >= 0) pad = env == 1;
+  if (pad) k_verify_sig<4, true><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
+  else k_verify_sig<4, true, false><<<nblk(n, 4), 64, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
 }
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s) {
   if (n > 0) k_gt_compare<<<n, 64, 0, s>>>(fe, y, n, codes);

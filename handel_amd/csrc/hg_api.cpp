@@ -297,6 +297,8 @@ struct hg_lane {
   hipEvent_t done = nullptr;
   bool recorded = false;  // `done` marks the lane's last batch
   bool overlap = true;    // the fold beside the pairing kernel (on ws.side)
+  bool pad = true;        // one pairing wave per SIMD (hg_lane_set_pairing_padding)
+  hipEvent_t ev_in = nullptr;  // hg_lane_submit_device: the caller's stream point
   size_t max_batch = 0, max_words = 0;
   uint8_t* h_in = nullptr;     // pinned staging
   int32_t* h_codes = nullptr;  // pinned
@@ -908,7 +910,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
       // side: wait -> prologue (codes, counters), plan, chunks, combine -> join
       HG_CHECK(c, hipEventRecord(ws.ev_fork, s));
       PhaseTimer t(c, HG_PHASE_VERIFY, s);
-      launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s);
+      launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s, lane ? lane->pad : true);
       t.stop();
       HG_CHECK(c, hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
       launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, ws.pts1.p, d_codes, (int*)gw.hdr,
@@ -1732,6 +1734,7 @@ int hg_lane_create(hg_ctx* c, size_t max_batch, size_t max_words, int overlap, h
                        ((max_batch * 64 + 255) & ~(size_t)255) + max_words * 8 + 256;
   hipError_t e = hipStreamCreateWithFlags(&l->s, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&l->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&l->ev_in, hipEventDisableTiming);
   if (e == hipSuccess) e = hipHostMalloc(&l->h_in, bytes, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc(&l->h_codes, max_batch * sizeof(int32_t), hipHostMallocDefault);
   if (e == hipSuccess) e = l->d_in.ensure(bytes);
@@ -1766,6 +1769,7 @@ int hg_lane_create(hg_ctx* c, size_t max_batch, size_t max_words, int overlap, h
     if (l->h_in) (void)hipHostFree(l->h_in);
     if (l->h_codes) (void)hipHostFree(l->h_codes);
     if (l->done) (void)hipEventDestroy(l->done);
+    if (l->ev_in) (void)hipEventDestroy(l->ev_in);
     if (l->s) (void)hipStreamDestroy(l->s);
     delete l;
     return HG_ERR_DEVICE;
@@ -1793,6 +1797,7 @@ void hg_lane_destroy(hg_lane* l) {
   (void)hipHostFree(l->h_in);
   (void)hipHostFree(l->h_codes);
   (void)hipEventDestroy(l->done);
+  (void)hipEventDestroy(l->ev_in);
   (void)hipStreamDestroy(l->s);
   delete l;
 }
@@ -1838,6 +1843,35 @@ int hg_lane_submit(hg_lane* l) {
   HG_CHECK(c, hipEventRecord(l->done, l->s));
   l->recorded = true;
   (void)hipStreamQuery(l->s);  // flush: start now
+  return HG_OK;
+}
+
+int hg_lane_set_pairing_padding(hg_lane* l, int pad) {
+  if (!l) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(l->c->mu);
+  l->pad = pad != 0;
+  return HG_OK;
+}
+
+int hg_lane_submit_device(hg_lane* l, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                          const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_bits, void* stream) {
+  if (!l || !d_reqs || !d_sigs || !d_codes || n == 0 || n > l->max_batch) return HG_ERR_ARG;
+  hg_ctx* c = l->c;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  hipStream_t caller = stream ? (hipStream_t)stream : c->stream;
+  // after the caller's earlier work on `stream` (its inputs, its last reads of
+  // d_codes / d_bits) and the context's last submission
+  HG_CHECK(c, hipEventRecord(l->ev_in, caller));
+  HG_CHECK(c, hipStreamWaitEvent(l->s, l->ev_in, 0));
+  if (c->last_ev) HG_CHECK(c, hipStreamWaitEvent(l->s, c->last_ev, 0));
+  const FoldCaps caps = fold_caps_worst(c, n);  // the device words are not visible to the host
+  int rc = aggregate_device_locked(c, d_reqs, n, d_words, d_sigs, d_codes, nullptr, nullptr, true, l->s, &caps,
+                                   d_bits, l);
+  if (rc) return rc;
+  HG_CHECK(c, hipEventRecord(l->done, l->s));
+  l->recorded = true;
+  HG_CHECK(c, hipStreamWaitEvent(caller, l->done, 0));  // the verdicts, in the caller's stream order
   return HG_OK;
 }
 

@@ -415,5 +415,45 @@ class Batcher:
         return b.value, r.value
 
 
+class DeviceLane:
+    """One hg_lane of an engine for batches already in HBM
+    (hg_lane_submit_device): each lane has its own streams and workspaces over
+    the engine's one registry and table set, so several lanes keep several
+    batches in flight. pad=False: the unpadded pairing kernel (two batches'
+    waves share the SIMDs). The engine must outlive the lane."""
+
+    def __init__(self, engine: Engine, max_batch: int, pad: bool = True, overlap: bool = True):
+        self.engine = engine
+        self.L = engine.L
+        h = ctypes.c_void_p()
+        # staging capacity for host batches: 64 words (4096 bits) per request
+        rc = self.L.hg_lane_create(engine.ctx, max_batch, max_batch * 64, 1 if overlap else 0, ctypes.byref(h))
+        if rc != 0:
+            raise HandelGPUError(f"hg_lane_create: code {rc}")
+        self.h = h
+        if not pad:
+            engine._check(self.L.hg_lane_set_pairing_padding(self.h, 0), "hg_lane_set_pairing_padding")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.hg_lane_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit_device(self, d_reqs: int, n: int, d_words: int, d_sigs: int, d_codes: int, d_bits: int = 0,
+                      stream: int = 0):
+        """Enqueues the batch after `stream`'s earlier work; `stream` waits for its verdicts."""
+        self.engine._check(self.L.hg_lane_submit_device(self.h, d_reqs, n, d_words, d_sigs, d_codes, d_bits or None,
+                                                        stream or None), "hg_lane_submit_device")
+
+    def wait(self):
+        self.engine._check(self.L.hg_lane_wait(self.h), "hg_lane_wait")
+
+
 def requests_array(items: Sequence[Tuple[int, int, int, int]]) -> np.ndarray:
     return np.array(items, dtype=REQ_DTYPE)

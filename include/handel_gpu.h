@@ -376,6 +376,18 @@ int hg_lane_query(hg_lane* lane);
 int hg_lane_wait(hg_lane* lane);
 /* The last batch's n codes (pinned host memory, valid once it is done). */
 const int32_t* hg_lane_codes(hg_lane* lane);
+/* A batch already in HBM through the lane (the device twin of
+ * hg_verify_aggregate_device_bits): enqueued on the lane's streams after the
+ * caller's earlier work on `stream` (NULL: the context's stream), and `stream`
+ * waits for the verdicts, so the caller reads d_codes / d_bits in its own
+ * stream order while the next batch runs on another lane. d_bits may be NULL.
+ * hg_lane_codes does not apply; hg_lane_query / hg_lane_wait do. */
+int hg_lane_submit_device(hg_lane* lane, const hg_request* d_reqs, size_t n, const uint64_t* d_words,
+                          const uint8_t* d_sigs, int32_t* d_codes, uint8_t* d_bits, void* stream);
+/* 1 (the default): the lane's pairing kernel holds one wave per SIMD (the
+ * lowest latency for one batch); 0: unpadded, so two batches in flight put
+ * two pairing waves on a SIMD (throughput of a continuous stream). */
+int hg_lane_set_pairing_padding(hg_lane* lane, int pad);
 /* Builds the GT tables of the current message up to `level` (0..2, capped as
  * hg_prepare_aggregate caps) now; for owners of lanes that follow the volume
  * policy themselves. Synchronous. */

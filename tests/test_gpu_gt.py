@@ -484,3 +484,47 @@ def test_fused_bitset_matches_pack(level, overlap):
         assert e.aggregate_tables() == level
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("pad", [False, True], ids=["unpadded", "padded"])
+def test_device_lanes_keep_batches_in_flight(pad):
+    """hg_lane_submit_device (bench.py's headline): two lanes of one context
+    alternate on a batch resident in HBM, each on its own torch stream, two
+    batches in flight; every round's codes are the expected verdicts (the
+    oracle's: test_gt_and_g2_paths_agree) and its bitset packs them."""
+    import torch
+
+    import bench
+    from handel_amd.distributed import pack_verdicts
+    from handel_amd.engine import DeviceLane
+
+    dev = torch.device("cuda", 0)
+    e = Engine(device=0, flavor="go")
+    lanes = []
+    try:
+        assert e.set_message(bench.LIB_MESSAGE) == 0
+        reqs, words, sigs, expect, _, reg = bench.make_aggregate_batch(e, 1000, 1024, seed=5)
+        assert e.prepare_aggregate() == 0
+        n = len(reqs)
+        d_reqs, d_words = bench._dev_bytes(reqs.tobytes(), dev), bench._dev_bytes(words.tobytes(), dev)
+        d_sigs = bench._dev_bytes(bytes(sigs), dev)
+        lanes = [DeviceLane(e, n, pad=pad) for _ in range(2)]
+        streams = [torch.cuda.Stream(dev) for _ in lanes]
+        codes = [torch.full((n,), -1, dtype=torch.int32, device=dev) for _ in lanes]
+        bits = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev) for _ in lanes]
+        for rnd in range(6):
+            i = rnd % 2
+            with torch.cuda.stream(streams[i]):
+                if rnd >= 2:  # the previous round of this lane was read: rewrite the outputs
+                    codes[i].fill_(-1)
+                lanes[i].submit_device(d_reqs.data_ptr(), n, d_words.data_ptr(), d_sigs.data_ptr(),
+                                       codes[i].data_ptr(), bits[i].data_ptr(), streams[i].cuda_stream)
+                got = codes[i].cpu().numpy()  # in the stream's order: after the lane's verdicts
+            assert np.array_equal(got, expect), (pad, rnd)
+            assert torch.equal(bits[i], pack_verdicts(codes[i])), (pad, rnd)
+        # the context's own submissions wait for the lanes' batches
+        assert list(e.verify_aggregate(reqs, words, sigs)) == list(expect)
+    finally:
+        for ln in lanes:
+            ln.close()
+        e.close()

@@ -30,7 +30,7 @@ def dispatches(d):
 
 def main():
     d = sys.argv[1]
-    anchor = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"k_verify_sig<4, true>")
+    anchor = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"k_verify_sig<4, true(, (true|false))?>")
     cols, rows = dispatches(d)
     print("columns:", ",".join(cols))
     idx = [i for i, r in enumerate(rows) if anchor.search(r[0])]
