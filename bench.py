@@ -729,6 +729,12 @@ def main():
     ap.add_argument("--prewarm", type=float, default=0.3,
                     help="seconds of untimed headline steps before the warmup steps (GPU clocks settle)")
     args = ap.parse_args()
+    # every HIP stream on a hardware queue of its own (the lanes' pairing and
+    # fold streams, the per-lane torch streams, the context's and the pipelined
+    # line's): sharing queues serialises one lane's kernels behind another's.
+    # Read when the HIP runtime starts (the first device call below).
+    if args.inflight > 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, 3 * args.inflight + 4))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1003,6 +1009,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "batches_in_flight": inflight,
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
             "prewarm": {"seconds": args.prewarm, "steps": prewarm_steps, "what": "untimed headline steps before the "
                         "warmup steps (GPU clocks settled whatever the warmup count)"},
