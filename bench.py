@@ -733,8 +733,11 @@ def main():
     # fold streams, the per-lane torch streams, the context's and the pipelined
     # line's): sharing queues serialises one lane's kernels behind another's.
     # Read when the HIP runtime starts (the first device call below).
-    if args.inflight > 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, 3 * args.inflight + 4))
+    # (the box presets 4: raised, never lowered; HG_BENCH_HW_QUEUES forces a value)
+    want_q = int(os.environ.get("HG_BENCH_HW_QUEUES", "0")) or (min(16, 3 * args.inflight + 4) if args.inflight > 1
+                                                                 else 0)
+    if want_q and (os.environ.get("HG_BENCH_HW_QUEUES") or int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) < want_q):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
