@@ -11,11 +11,12 @@ bitset of density U[0.5, 1], the aggregate signature of the set bits, 1/8 of
 the aggregates tampered. Inputs (requests, bitset words, signatures) are
 resident in HBM; verdict codes are written to HBM, packed into a bitset and
 all-gathered over RCCL (the only cross-GPU traffic). The verifier serves a
-continuous stream of such batches: two are in flight at a time on the
+continuous stream of such batches: four are in flight at a time on the
 context's lanes (hg_lane_submit_device: own streams and workspaces over the
 one registry and table set, the unpadded pairing kernel), so one batch's
-pairing waves share the SIMDs with the next one's (--inflight 1: one batch at
-a time, the `sequential` sub-line).
+pairing waves share the SIMDs with the next one's and each batch's fold,
+comparison and launch gaps hide behind the others' pairing kernels
+(--inflight 1: one batch at a time, the `sequential` sub-line).
 
 Sub-lines (never `value`):
   sequential      the headline batch one at a time on the context's stream
@@ -718,7 +719,7 @@ def main():
                     help="config 5: each rank is one committee of 4096 signers (own 4096-key registry)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="headline only (no single / full / pipelined lines)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="headline: batches in flight on the context's lanes (1: one batch at a time on the "
                          "context's stream)")
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight for the 'pipelined' line (1: skip)")
