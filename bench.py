@@ -719,9 +719,9 @@ def main():
                     help="config 5: each rank is one committee of 4096 signers (own 4096-key registry)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="headline only (no single / full / pipelined lines)")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="headline: batches in flight on the context's lanes (1: one batch at a time on the "
-                         "context's stream)")
+                         "context's stream; default 4, 3 per rank with RCCL)")
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight for the 'pipelined' line (1: skip)")
     ap.add_argument("--pipeline-overlap", type=int, default=1,
                     help="the pipelined line's contexts run their fold beside the pairing kernel (1) or before it (0)")
@@ -730,6 +730,8 @@ def main():
     ap.add_argument("--prewarm", type=float, default=0.3,
                     help="seconds of untimed headline steps before the warmup steps (GPU clocks settle)")
     args = ap.parse_args()
+    if args.inflight is None:  # RCCL's stream takes one of the 16 hardware queues below
+        args.inflight = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
     # every HIP stream on a hardware queue of its own (the lanes' pairing and
     # fold streams, the per-lane torch streams, the context's and the pipelined
     # line's): sharing queues serialises one lane's kernels behind another's.
