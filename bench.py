@@ -730,8 +730,14 @@ def main():
     ap.add_argument("--prewarm", type=float, default=0.3,
                     help="seconds of untimed headline steps before the warmup steps (GPU clocks settle)")
     args = ap.parse_args()
-    if args.inflight is None:  # RCCL's stream takes one of the 16 hardware queues below
-        args.inflight = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
+    if args.inflight is None:
+        # RCCL's stream takes one of the 16 hardware queues below; the gloo
+        # rehearsal (ranks sharing a GPU) runs one batch at a time per rank, so
+        # the processes on one device stay within 16 queues together
+        if os.environ.get("HG_BENCH_BACKEND", "nccl") == "gloo":
+            args.inflight = 1
+        else:
+            args.inflight = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
     # every HIP stream on a hardware queue of its own (the lanes' pairing and
     # fold streams, the per-lane torch streams, the context's and the pipelined
     # line's): sharing queues serialises one lane's kernels behind another's.
