@@ -743,8 +743,10 @@ def main():
     # line's): sharing queues serialises one lane's kernels behind another's.
     # Read when the HIP runtime starts (the first device call below).
     # (the box presets 4: raised, never lowered; HG_BENCH_HW_QUEUES forces a value)
-    want_q = int(os.environ.get("HG_BENCH_HW_QUEUES", "0")) or (min(16, 3 * args.inflight + 4) if args.inflight > 1
-                                                                 else 0)
+    # (per lane: the pairing and fold streams, plus a torch stream with RCCL)
+    per_lane = 2 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
+    want_q = int(os.environ.get("HG_BENCH_HW_QUEUES", "0")) or (min(16, per_lane * args.inflight + 4)
+                                                                 if args.inflight > 1 else 0)
     if want_q and (os.environ.get("HG_BENCH_HW_QUEUES") or int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) < want_q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
@@ -801,13 +803,20 @@ def main():
             bits_i = head.d_bits if i == 0 else torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
             gath_i = gathered if i == 0 else [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev)
                                               for _ in range(world)]
-            lane_out.append((torch.cuda.Stream(dev), codes_i, bits_i, gath_i))
+            lane_out.append((torch.cuda.Stream(dev) if world > 1 else None, codes_i, bits_i, gath_i))
     turn = [0]
 
     def lane_step():
         i = turn[0] % inflight
         turn[0] += 1
         st, codes_i, bits_i, gath_i = lane_out[i]
+        if world == 1:
+            # nothing reads the verdicts between steps (the gather is the
+            # identity): the lane orders each batch after its own previous one
+            lanes[i].submit_device(head.d_reqs.data_ptr(), n, head.d_words.data_ptr(), head.d_sigs.data_ptr(),
+                                   codes_i.data_ptr(), bits_i.data_ptr(), lanes[i].stream)
+            gather_verdicts(bits_i, world, gath_i)
+            return
         with torch.cuda.stream(st):
             lanes[i].submit_device(head.d_reqs.data_ptr(), n, head.d_words.data_ptr(), head.d_sigs.data_ptr(),
                                    codes_i.data_ptr(), bits_i.data_ptr(), st.cuda_stream)

@@ -117,6 +117,7 @@ SIGNATURES = {
     "hg_lane_codes": (ctypes.POINTER(ctypes.c_int32), [_P]),
     "hg_lane_submit_device": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
     "hg_lane_set_pairing_padding": (_I, [_P, _I]),
+    "hg_lane_stream": (_P, [_P]),
     "hg_service_config_init": (None, [_P]),
     "hg_service_create": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_P)]),
     "hg_service_create_echo": (_I, [ctypes.c_char_p, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_P)]),

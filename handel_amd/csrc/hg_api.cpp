@@ -1846,6 +1846,8 @@ int hg_lane_submit(hg_lane* l) {
   return HG_OK;
 }
 
+void* hg_lane_stream(hg_lane* l) { return l ? (void*)l->s : nullptr; }
+
 int hg_lane_set_pairing_padding(hg_lane* l, int pad) {
   if (!l) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(l->c->mu);

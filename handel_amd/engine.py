@@ -454,6 +454,12 @@ class DeviceLane:
     def wait(self):
         self.engine._check(self.L.hg_lane_wait(self.h), "hg_lane_wait")
 
+    @property
+    def stream(self) -> int:
+        """The lane's launch stream (hipStream_t as int): as submit_device's
+        `stream`, the batch is ordered only after the lane's own earlier ones."""
+        return int(self.L.hg_lane_stream(self.h) or 0)
+
 
 def requests_array(items: Sequence[Tuple[int, int, int, int]]) -> np.ndarray:
     return np.array(items, dtype=REQ_DTYPE)

@@ -388,6 +388,9 @@ int hg_lane_submit_device(hg_lane* lane, const hg_request* d_reqs, size_t n, con
  * lowest latency for one batch); 0: unpadded, so two batches in flight put
  * two pairing waves on a SIMD (throughput of a continuous stream). */
 int hg_lane_set_pairing_padding(hg_lane* lane, int pad);
+/* The lane's launch stream (a hipStream_t): passed as hg_lane_submit_device's
+ * `stream`, the lane orders its batches only after its own earlier ones. */
+void* hg_lane_stream(hg_lane* lane);
 /* Builds the GT tables of the current message up to `level` (0..2, capped as
  * hg_prepare_aggregate caps) now; for owners of lanes that follow the volume
  * policy themselves. Synchronous. */
