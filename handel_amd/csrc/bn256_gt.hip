@@ -775,11 +775,13 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
 
 // team_final_exp_fc (bn256_pairing.h) on layout S: the same chain over seven
 // slots F, A, B, C, D, E, G (the full layout spreads it over eleven), so the
-// team region is 120 elements instead of 180 and two pairing waves fit on a
-// SIMD's share of the LDS. Slot roles: F = res; the easy part's inversion
+// team region is 118 elements instead of 180: eight pairing waves and a fold
+// workgroup fit in a CU's LDS. Slot roles: F = res; the easy part's inversion
 // uses D, E; the exponentiations by v ping-pong D <-> E with the base's
 // conjugate in G; t0 = A, t1 = B, t2 = C, t4 = G, t3 = B (once t1 is
-// consumed); D carries the Frobenius temporaries of the last products.
+// consumed); D carries the Frobenius temporaries of the last products. The
+// next base t2^2 is a product, not the canonical cyclotomic squaring, whose
+// pre-pass scratch would end the region 2 elements later.
 HG_DEV constexpr XHint final_exp_hint_s() { return xh<IMul12S<S_E, S_F, S_D>>(); }
 HG_DEV void team_final_exp_fc_s(const Team& T, XStream& S) {
   // easy part: res = f^((p^6 - 1)(p^2 + 1)), f^-1 = conj(f) / (f conj(f))
@@ -811,8 +813,8 @@ HG_DEV void team_final_exp_fc_s(const Team& T, XStream& S) {
     } else if (ph == 1) {  // t2 = conj(t1^u), t1 = t2 conj(t1); next base t3 = t2^2
       t12_conj(T, S_C, S_E);
       t12_conj(T, S_G, S_B);
-      IMul12S<S_B, S_C, S_G>::run(T, S, xh<ICyc0S<S_D, S_C>>());
-      ICyc0S<S_D, S_C>::run(T, S, xh<ICycS<S_E, S_D>>());
+      IMul12S<S_B, S_C, S_G>::run(T, S, xh<IMul12S<S_D, S_C, S_C>>());
+      IMul12S<S_D, S_C, S_C>::run(T, S, xh<ICycS<S_E, S_D>>());  // canonical (feeds a conj)
     } else {  // t4 = t1 t3^u
       IMul12S<S_G, S_B, S_E>::run(T, S, xh<IMul12S<S_B, S_A, S_G>>());
     }
@@ -847,9 +849,9 @@ HG_DEV bool t12_equal(const Team& T, int a, int b) {
 // beside this kernel on a second stream; k_gt_compare finishes the check)
 // The team region is layout S (kSigTeamElems, from the generator: slots F..G,
 // then the registers from kSigRegBase, the FE pre-pass scratch among them):
-// 19.2 KB of LDS per 4-team wave instead of k_verify's 33.9 KB, so the CU's
+// 18.9 KB of LDS per 4-team wave instead of k_verify's 33.9 KB, so the CU's
 // LDS holds its four pairing waves and the fold's workgroups beside them, or
-// eight pairing waves.
+// eight pairing waves (two batches in flight) and a fold workgroup.
 static constexpr int kSigTeamWords = kSigTeamElems * 10;
 static_assert(kSigTeamWords % 2 == 0 && kSigTeamWords <= kTeamWords, "sig team region");
 // kStore: the signature is decoded here from its marshal (sig_bytes, the

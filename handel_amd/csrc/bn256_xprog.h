@@ -457,8 +457,6 @@ template <int D, int A, int B>
 using IMul12S = XInst<XP_MUL12_S, D, A, B>;
 template <int D, int A>
 using ICycS = XInst<XP_CYC_SQR_X_S, D, A>;
-template <int D, int A>
-using ICyc0S = XInst<XP_CYC_SQR_S, D, A>;  // canonical result
 
 // t12_pow_v_x on layout S: dst = a^v with the conjugate of a in slot SK
 template <int D, int SA, int SK>

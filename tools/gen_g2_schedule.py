@@ -1169,8 +1169,9 @@ INSTANCES = sorted(set(
 # exponentiation (team_final_exp_fc_s) need no more — then the register file.
 # The Miller loop's pre-pass scratch lies in slots A.. (only F is live there),
 # the final exponentiation's past register ONE (the Miller registers are dead
-# there), as in the full layout. 120 elements per team instead of 180: 19.2 KB
-# of LDS per 4-team wave, so two pairing waves fit on a SIMD.
+# there), as in the full layout. 118 elements per team instead of 180: 18.9 KB
+# of LDS per 4-team wave, so two pairing waves fit on a SIMD and the CU keeps
+# room for a fold workgroup beside its eight pairing waves.
 SIG_SLOTS = SLOTS[:7]
 SIG_F_BASE = 12 * len(SIG_SLOTS)
 SIG_SCR_BASE = {"FE": SIG_F_BASE + 2, "ML": 12 * SLOTS.index("A")}
@@ -1183,7 +1184,9 @@ SIG_INSTANCES = sorted(set(
                               ("B", "A", "B"), ("B", "C", "G"), ("G", "B", "E"), ("B", "A", "G"),
                               ("A", "C", "G"), ("A", "F", "A"), ("A", "D", "A"), ("D", "D", "B"), ("F", "D", "A")]]
     + [("CYC_SQR_X", b) for b in [("E", "D"), ("E", "E"), ("D", "E"), ("D", "D"), ("A", "A"), ("B", "A")]]
-    + [("CYC_SQR", ("D", "C"))]))
+    # t3 = t2^2 as a product (canonical, 21 scratch elements: the canonical
+    # CYC_SQR's 34 would set the region's end)
+    + [("MUL12", ("D", "C", "C"))]))
 ALL_INSTANCES = [(n, b, "") for n, b in INSTANCES] + [(n, b, "S") for n, b in SIG_INSTANCES]
 
 
