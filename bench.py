@@ -709,6 +709,12 @@ def roofline(fpmul: int, ms: float, kernel: str, traffic_pattern: str, work: str
     return out
 
 
+def progress(what: str):
+    """One line per phase on stderr (the JSON line stays alone on stdout): a
+    long run under a profiler shows it is alive."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {what}", file=sys.stderr, flush=True)
+
+
 def lanes_rate(eng: Engine, wl, inflight: int, timer, steps: int, warmup: int, dev) -> float:
     """wl's batch with `inflight` batches in flight on the context's lanes, as
     the headline runs (unpadded pairing kernel, each lane ordered on its own
@@ -856,6 +862,7 @@ def main():
     for codes_i in ([o[1] for o in lane_out] if lanes else [head.d_codes]):
         head.check(codes_i)
     assert torch.equal(head.d_bits, pack_verdicts(head.d_codes)), "HIP verdict bitset differs from the codes"
+    progress(f"headline: {inflight} in flight, prewarm / warmup / {args.steps} timed steps")
     prewarm_steps = timer.prewarm(step, args.prewarm)
     dt = timer.run(step, args.steps, args.warmup)
     rank_ms = [round(t / args.steps * 1e3, 4) for t in timer.rank_times]
@@ -873,6 +880,7 @@ def main():
     for ln in lanes:
         ln.close()
     sequential = None
+    progress("headline done; sequential, per-kernel phases")
     if inflight > 1 and not args.no_extra:
         sdt_seq = timer.run(seq_step, args.steps, args.warmup)
         head.check()
@@ -939,6 +947,7 @@ def main():
                                 "submit": round(ph_seq["submit"], 4)}
 
     extra = {}
+    progress("sub-lines")
     if not args.no_extra:
         # config 2: independent single-signature checks
         single = SingleWorkload(eng, n, seed=1234 + rank, dev=dev, stream=stream)
@@ -984,6 +993,7 @@ def main():
 
         rdt = timer.run(rstep, args.steps, args.warmup)
         assert np.array_equal(rcodes.cpu().numpy(), rexpect), "registry single-signature verdicts"
+        progress("single_registry")
         extra["single_registry"] = {
             "metric": "BN254 single-sig verifications/sec, registry keys (batch 4096)",
             "value": round(n * args.steps * world / rdt, 1), "unit": "verifications/s",
@@ -1001,6 +1011,7 @@ def main():
             full_inflight = {"value": round(n * args.steps * world / idt, 1), "unit": "verifications/s",
                              "ms_per_step": round(idt / args.steps * 1e3, 4), "batches_in_flight": inflight,
                              "what": "the same batches in flight on the context's lanes, as the headline runs"}
+        progress("full_registry")
         extra["full_registry"] = {
             "metric": "BN254 aggregate-sig verifications/sec (VerifyMultiSignature over the registry)",
             "value": round(n * args.steps * world / fdt, 1), "unit": "verifications/s",
@@ -1039,6 +1050,7 @@ def main():
             pdt = timer.run(pstep, args.steps, args.warmup)
             for cd in codes_p:
                 head.check(cd)
+            progress("pipelined")
             extra["pipelined"] = {"value": round(n * len(engs) * args.steps * world / pdt, 1),
                                   "unit": "verifications/s", "batches_in_flight": len(engs), "batch": n,
                                   "ms_per_step": round(pdt / args.steps * 1e3, 4),
@@ -1047,19 +1059,24 @@ def main():
                 e.close()
             eng.set_fold_overlap(True)
 
+        progress("packet_intake")
         extra["packet_intake"] = packet_intake(eng, head, n_reg, dev, stream, timer, args, world)
+        progress("batch_latency")
         extra["batch_latency"] = {
             "what": "one batch submitted alone and waited for (median of 15), first n headline requests: the "
                     "per-check latency floor a one-check-at-a-time evaluator (processing.go:228-287) sees",
             **batch_latency(eng, head, dev)}
+        progress("handel_run_volume")
         extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)
         if rank == 0 and world == 1 and not args.no_service:
-            extra["config4_proxy"] = {
+            progress("config4_proxy")
+        extra["config4_proxy"] = {
                 "what": "simul's 2000-node single-host verification load (8 processes x 250 instances x 45 checks, "
                         "one check in flight per instance) on this GPU; checks/s, per-check latency, HBM",
                 "service": config4_proxy("service"), "contexts": config4_proxy("contexts")}
 
     cpu = None
+    progress("CPU baseline" if rank == 0 and world == 1 and not args.no_cpu else "done")
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             cpu = cpu_baseline_aggregate(head.reg, head.reqs, head.words, head.sigs, head.expect, args.cpu_sample)
