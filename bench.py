@@ -414,6 +414,22 @@ class Timer:
         the GPU's clocks have settled whatever the warmup count; returns the
         steps run (reported in the line)."""
         k, t0 = 0, time.perf_counter()
+        if self.dist:
+            # every rank runs the same number of steps (a step holds a
+            # collective): the ranks agree after each step, and stop as soon
+            # as one rank's time is up
+            import torch.distributed as tdist
+
+            go = torch.ones(1, dtype=torch.int32, device=self.coll_dev)
+            while seconds > 0:
+                step()
+                k += 1
+                go.fill_(1 if time.perf_counter() - t0 < seconds else 0)
+                tdist.all_reduce(go, op=tdist.ReduceOp.MIN)
+                if int(go.item()) == 0:
+                    break
+            torch.cuda.synchronize(self.dev)
+            return k
         while time.perf_counter() - t0 < seconds:
             step()
             k += 1
