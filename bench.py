@@ -409,6 +409,10 @@ class Timer:
         self.dev, self.dist, self.coll_dev, self.world = dev, dist, coll_dev, world
         self.rank_times = []
 
+    def _sync(self):
+        if self.dev.type == "cuda":  # (a CPU device: the gloo test of this class)
+            torch.cuda.synchronize(self.dev)
+
     def prewarm(self, step, seconds: float) -> int:
         """Untimed steps for `seconds` of wall time before the warmup steps, so
         the GPU's clocks have settled whatever the warmup count; returns the
@@ -428,28 +432,28 @@ class Timer:
                 tdist.all_reduce(go, op=tdist.ReduceOp.MIN)
                 if int(go.item()) == 0:
                     break
-            torch.cuda.synchronize(self.dev)
+            self._sync()
             return k
         while time.perf_counter() - t0 < seconds:
             step()
             k += 1
             if k % 16 == 0:
-                torch.cuda.synchronize(self.dev)
-        torch.cuda.synchronize(self.dev)
+                self._sync()
+        self._sync()
         return k
 
     def run(self, step, steps: int, warmup: int) -> float:
         for _ in range(warmup):
             step()
-        torch.cuda.synchronize(self.dev)
+        self._sync()
         if self.dist:
             import torch.distributed as tdist
             tdist.barrier()
-        torch.cuda.synchronize(self.dev)
+        self._sync()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
-        torch.cuda.synchronize(self.dev)
+        self._sync()
         if self.dist:
             tdist.barrier()
         dt = time.perf_counter() - t0
