@@ -774,7 +774,7 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="headline only (no single / full / pipelined lines)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="headline: batches in flight on the context's lanes (1: one batch at a time on the "
-                         "context's stream; default 4, 3 per rank with RCCL)")
+                         "context's stream; default 4; 1 in the gloo rehearsal)")
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight for the 'pipelined' line (1: skip)")
     ap.add_argument("--pipeline-overlap", type=int, default=1,
                     help="the pipelined line's contexts run their fold beside the pairing kernel (1) or before it (0)")
@@ -784,21 +784,17 @@ def main():
                     help="seconds of untimed headline steps before the warmup steps (GPU clocks settle)")
     args = ap.parse_args()
     if args.inflight is None:
-        # RCCL's stream takes one of the 16 hardware queues below; the gloo
-        # rehearsal (ranks sharing a GPU) runs one batch at a time per rank, so
-        # the processes on one device stay within 16 queues together
-        if os.environ.get("HG_BENCH_BACKEND", "nccl") == "gloo":
-            args.inflight = 1
-        else:
-            args.inflight = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
+        # the gloo rehearsal (ranks sharing a GPU) runs one batch at a time per
+        # rank, so the processes on one device stay within 16 queues together
+        args.inflight = 1 if os.environ.get("HG_BENCH_BACKEND", "nccl") == "gloo" else 4
     # every HIP stream on a hardware queue of its own (the lanes' pairing and
     # fold streams, the per-lane torch streams, the context's and the pipelined
     # line's): sharing queues serialises one lane's kernels behind another's.
     # Read when the HIP runtime starts (the first device call below).
     # (the box presets 4: raised, never lowered; HG_BENCH_HW_QUEUES forces a value)
-    # (per lane: the pairing and fold streams, plus a torch stream with RCCL)
-    per_lane = 2 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
-    want_q = int(os.environ.get("HG_BENCH_HW_QUEUES", "0")) or (min(16, per_lane * args.inflight + 4)
+    # (per lane: its pairing and fold streams; the gather runs on the lane's
+    # own stream; + the context's, torch's and RCCL's)
+    want_q = int(os.environ.get("HG_BENCH_HW_QUEUES", "0")) or (min(16, 2 * args.inflight + 4)
                                                                  if args.inflight > 1 else 0)
     if want_q and (os.environ.get("HG_BENCH_HW_QUEUES") or int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) < want_q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
@@ -856,7 +852,10 @@ def main():
             bits_i = head.d_bits if i == 0 else torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
             gath_i = gathered if i == 0 else [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=coll_dev)
                                               for _ in range(world)]
-            lane_out.append((torch.cuda.Stream(dev) if world > 1 else None, codes_i, bits_i, gath_i))
+            # the gather runs on the lane's own stream (wrapped for torch), right
+            # after the lane's verdicts; the lane's next batch follows it there
+            lane_out.append((torch.cuda.ExternalStream(lanes[-1].stream, device=dev) if world > 1 else None,
+                             codes_i, bits_i, gath_i))
     turn = [0]
 
     def lane_step():
@@ -872,7 +871,7 @@ def main():
             return
         with torch.cuda.stream(st):
             lanes[i].submit_device(head.d_reqs.data_ptr(), n, head.d_words.data_ptr(), head.d_sigs.data_ptr(),
-                                   codes_i.data_ptr(), bits_i.data_ptr(), st.cuda_stream)
+                                   codes_i.data_ptr(), bits_i.data_ptr(), lanes[i].stream)
             gather_verdicts(bits_i.to(coll_dev), world, gath_i)
 
     step = lane_step if inflight > 1 else seq_step
