@@ -927,7 +927,7 @@ def main():
                     (f"the GT submission, {inflight} batches in flight (timed region per step): " if inflight > 1
                      else "the GT submission: ") + "k_agg_prologue, k_verify_sig beside the GT fold (k_gt_plan, "
                     "k_gt_chunks, k_gt_combine), k_gt_compare_bits",
-                    r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare_bits)|k_verify_sig<4, true(, (true|false))?>",
+                    r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare_bits)|" + sig_kernel,
                     f"implemented work: {head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 "
                     f"product each) + {n} x {FPMUL_PER_SIG_PAIRING} Fp-mul (one pairing + final exponentiation "
                     f"per check), x {MADS_PER_FPMUL} u32 mads",
