@@ -695,6 +695,12 @@ def config4_proxy(model: str, timeout: int = 180):
     return {k: d[k] for k in keep if k in d}
 
 
+def want_config4_proxy(rank: int, world: int, args) -> bool:
+    """The config-4 proxy line runs on a one-rank run only (rank 0, world 1),
+    and never with --no-service or --no-extra."""
+    return rank == 0 and world == 1 and not args.no_service and not args.no_extra
+
+
 def timed_phases(eng: Engine, run):
     """Runs run() with the engine's HIP-event timing on; returns per-phase
     (mean ms per interval) for verify / aggregate fold / whole submission."""
@@ -762,9 +768,48 @@ def lanes_rate(eng: Engine, wl, inflight: int, timer, steps: int, warmup: int, d
     return dt
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` outside torchrun: start N rank processes (one
+    per GPU) as a CHILD torch.distributed.run on 127.0.0.1 with the same
+    arguments, and return its exit code. Called before any HIP call of this
+    process (nothing here touches the device), and the ranks are fresh
+    processes, never an exec of this one."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    progress(f"launching {n} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd, env=dict(os.environ, HG_BENCH_LAUNCHED="1"))
+
+
+def world_from_env(gpus):
+    """(world, rank, local rank) of this process; SystemExit(2) when --gpus
+    names a different world size than the launcher started (the line's n_gpus
+    would otherwise not be what was asked for)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if gpus is not None and gpus != world:
+        print(f"bench.py: --gpus {gpus} but the launcher started a world of {world} rank(s)", file=sys.stderr)
+        raise SystemExit(2)
+    return world, rank, local
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; outside torchrun N > 1 starts N ranks itself")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="test hook: start the ranks, join the process group (gloo, no device), print the "
+                         "world each rank saw, exit")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=4096)
@@ -783,6 +828,24 @@ def main():
     ap.add_argument("--prewarm", type=float, default=0.3,
                     help="seconds of untimed headline steps before the warmup steps (GPU clocks settle)")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # the driver's `python bench.py --gpus N`: one rank per GPU, started here
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = world_from_env(args.gpus)
+    if args.launch_probe:
+        import torch.distributed as tdist
+
+        if world > 1:
+            tdist.init_process_group("gloo")
+        seen = tdist.get_world_size() if world > 1 else 1
+        ranks = [None] * world
+        if world > 1:
+            tdist.all_gather_object(ranks, rank)
+            tdist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "world_size_seen": seen, "ranks": ranks if world > 1 else [0],
+                              "launched": os.environ.get("HG_BENCH_LAUNCHED") == "1"}))
+        return
     if args.inflight is None:
         # the gloo rehearsal (ranks sharing a GPU) runs one batch at a time per
         # rank, so the processes on one device stay within 16 queues together
@@ -799,9 +862,6 @@ def main():
     if want_q and (os.environ.get("HG_BENCH_HW_QUEUES") or int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) < want_q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     # HG_BENCH_BACKEND=gloo is a rehearsal mode for boxes with fewer GPUs than
     # ranks (ranks share devices round-robin, collectives on host copies); the
@@ -1087,9 +1147,11 @@ def main():
             **batch_latency(eng, head, dev)}
         progress("handel_run_volume")
         extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)
-        if rank == 0 and world == 1 and not args.no_service:
+        if want_config4_proxy(rank, world, args):
+            # one GPU's line: the proxy's processes open device 0 (single-host
+            # simul on one GPU), so it never runs beside other ranks
             progress("config4_proxy")
-        extra["config4_proxy"] = {
+            extra["config4_proxy"] = {
                 "what": "simul's 2000-node single-host verification load (8 processes x 250 instances x 45 checks, "
                         "one check in flight per instance) on this GPU; checks/s, per-check latency, HBM",
                 "service": config4_proxy("service"), "contexts": config4_proxy("contexts")}

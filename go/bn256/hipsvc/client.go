@@ -45,9 +45,17 @@ type Client struct {
 	mu      sync.Mutex
 	waiting map[uint64]chan int32
 	early   map[uint64]int32 // codes collected before their waiter registered
-	done    chan struct{}
+	done    chan struct{}    // closed by Close: poll returns
+	polled  chan struct{}    // closed by poll when it returns
 	dead    error
+	// hmu guards the handle itself: submits hold it shared, Close exclusively,
+	// so hg_client_close never runs while a C call uses the handle
+	hmu       sync.RWMutex
+	closed    bool
+	closeOnce sync.Once
 }
+
+var errClosed = errors.New("hipsvc: client closed")
 
 // Open attaches to the verifier region `name` (hg_verifierd --name).
 func Open(name string) (*Client, error) {
@@ -57,13 +65,15 @@ func Open(name string) (*Client, error) {
 	if rc := C.hg_client_open(cn, &h); rc != C.HG_OK {
 		return nil, fmt.Errorf("hipsvc: cannot attach to %s (code %d)", name, int(rc))
 	}
-	c := &Client{h: h, waiting: map[uint64]chan int32{}, early: map[uint64]int32{}, done: make(chan struct{})}
+	c := &Client{h: h, waiting: map[uint64]chan int32{}, early: map[uint64]int32{}, done: make(chan struct{}),
+		polled: make(chan struct{})}
 	go c.poll()
 	return c, nil
 }
 
 // poll collects finished tickets and delivers their codes.
 func (c *Client) poll() {
+	defer close(c.polled)
 	tickets := make([]C.uint64_t, 512)
 	codes := make([]C.int32_t, 512)
 	for {
@@ -74,13 +84,7 @@ func (c *Client) poll() {
 		default:
 		}
 		if n < 0 {
-			c.mu.Lock()
-			c.dead = errors.New("hipsvc: the verifier stopped")
-			for t, ch := range c.waiting {
-				ch <- -1
-				delete(c.waiting, t)
-			}
-			c.mu.Unlock()
+			c.failAll(errors.New("hipsvc: the verifier stopped"))
 			return
 		}
 		c.mu.Lock()
@@ -97,10 +101,35 @@ func (c *Client) poll() {
 	}
 }
 
-// Close detaches (tickets in flight are dropped).
+// failAll ends every registered waiter with err (they return it).
+func (c *Client) failAll(err error) {
+	c.mu.Lock()
+	if c.dead == nil {
+		c.dead = err
+	}
+	for t, ch := range c.waiting {
+		ch <- -1
+		delete(c.waiting, t)
+	}
+	c.mu.Unlock()
+}
+
+// Close detaches (tickets in flight are dropped; their Verify calls return
+// an error). The poll goroutine is stopped first — it may sit in
+// hg_client_wait_any for up to 100 ms — and no submit is in progress when
+// the handle is released (handel_client.h: close must not run concurrently
+// with the handle's other calls). Safe to call more than once.
 func (c *Client) Close() {
-	close(c.done)
-	C.hg_client_close(c.h)
+	c.closeOnce.Do(func() {
+		close(c.done)
+		<-c.polled
+		c.failAll(errClosed)
+		c.hmu.Lock()
+		c.closed = true
+		C.hg_client_close(c.h)
+		c.h = nil
+		c.hmu.Unlock()
+	})
 }
 
 func u8ptr(b []byte) *C.uint8_t {
@@ -127,8 +156,15 @@ func (c *Client) Verify(msg []byte, r Request) error {
 		words = (*C.uint64_t)(unsafe.Pointer(&r.Words[0]))
 	}
 	var t C.uint64_t
+	c.hmu.RLock()
+	if c.closed {
+		c.hmu.RUnlock()
+		return errClosed
+	}
 	// the library copies every input before returning (cgo pointer rules hold)
-	if rc := C.hg_client_submit(c.h, u8ptr(msg), C.size_t(len(msg)), &req, words, u8ptr(r.Sig), &t); rc != C.HG_OK {
+	rc := C.hg_client_submit(c.h, u8ptr(msg), C.size_t(len(msg)), &req, words, u8ptr(r.Sig), &t)
+	c.hmu.RUnlock()
+	if rc != C.HG_OK {
 		return fmt.Errorf("hipsvc: submit refused (code %d)", int(rc))
 	}
 	ch := make(chan int32, 1)
@@ -146,15 +182,24 @@ func (c *Client) Verify(msg []byte, r Request) error {
 	c.mu.Unlock()
 	code := <-ch
 	if code < 0 {
-		return errors.New("hipsvc: the verifier stopped")
+		c.mu.Lock()
+		err := c.dead
+		c.mu.Unlock()
+		return err
 	}
 	return c.codeError(code)
 }
 
-// codeError maps an hg_code to processing.go's error (nil for HG_OK).
+// codeError maps an hg_code to processing.go's error (nil for HG_OK). The
+// texts need no handle beyond the flavor (hg_client_processing_error_string).
 func (c *Client) codeError(code int32) error {
 	if code == C.HG_OK {
 		return nil
+	}
+	c.hmu.RLock()
+	defer c.hmu.RUnlock()
+	if c.closed {
+		return errClosed
 	}
 	return errors.New(C.GoString(C.hg_client_processing_error_string(c.h, C.int(code))))
 }

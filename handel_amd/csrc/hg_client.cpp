@@ -69,6 +69,7 @@ void drain_locked(hg_client* c) {
     c->order.push_back(t);
     s->state.store(kSlotFree, std::memory_order_release);
     fb[id / 64].fetch_or(1ull << (id % 64), std::memory_order_release);
+    c->chan->inflight.fetch_sub(1, std::memory_order_acq_rel);
   }
 }
 
@@ -205,6 +206,7 @@ int hg_client_open(const char* name, hg_client** out) {
     return HG_ERR_ARG;
   }
   c->chan = c->v.chan(c->ch);
+  // (a released channel owns no slot: inflight is 0)
   c->chan->pid = (uint32_t)getpid();
   c->head = c->chan->tail.load(std::memory_order_acquire);
   c->hint = (uint32_t)(c->ch * 7) % (h->nslots / 64);
@@ -219,10 +221,22 @@ void hg_client_close(hg_client* c) {
     drain_locked(c);  // frees the slots of finished, uncollected tickets
     for (const Pinned& p : c->pinned) c->v.h->msgs[p.id].refs.fetch_sub(1, std::memory_order_acq_rel);
     c->pinned.clear();
+    if (c->chan->inflight.load(std::memory_order_acquire) == 0) {
+      c->chan->used.store(kChanFree, std::memory_order_release);
+    } else {
+      // tickets still in flight: the channel stays reserved (a new handle
+      // would otherwise collect their completions) and the service frees
+      // their slots itself, from where this handle's drain stopped
+      Header* h = c->v.h;
+      c->chan->head = c->head;
+      c->chan->used.store(kChanOrphaned, std::memory_order_seq_cst);
+      h->orphans.fetch_add(1, std::memory_order_seq_cst);
+      if (h->sleeping.load(std::memory_order_seq_cst)) {
+        h->doorbell.fetch_add(1, std::memory_order_seq_cst);
+        futex_wake(&h->doorbell, 1);
+      }
+    }
   }
-  // a ticket still in flight keeps its slot until the service finishes it;
-  // the channel is reusable once its ring has caught up
-  c->chan->used.store(0, std::memory_order_release);
   munmap(c->v.base, c->bytes);
   delete c;
 }
@@ -243,8 +257,10 @@ int hg_client_submit(hg_client* c, const uint8_t* msg, size_t len, const hg_requ
     mgen = p->gen;
     p->outstanding++;
   }
+  c->chan->inflight.fetch_add(1, std::memory_order_acq_rel);  // before the slot can complete
   const int64_t id = claim_slot(c);
   if (id < 0) {
+    c->chan->inflight.fetch_sub(1, std::memory_order_acq_rel);
     std::lock_guard<std::mutex> g(c->mu);
     for (Pinned& p : c->pinned)
       if (p.id == mid && p.gen == mgen && p.outstanding) p.outstanding--;

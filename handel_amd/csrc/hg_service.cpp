@@ -151,8 +151,15 @@ struct EchoExec : Exec {
   int build_level(int) override { return HG_OK; }
 };
 
+// A queued request as intake() found it: every field the dispatcher uses is
+// copied out of the shared slot once, when the slot turns Taken, so a client
+// that rewrites its slot afterwards cannot change what is validated, sized or
+// copied (processing.go:342-352: a bitset that does not fit its level is an
+// error, never a crash). Only the bitset words and the signature are read from
+// the slot later, once, at launch, sized by this copy.
 struct Pending {
-  uint32_t slot, msg, msg_gen;
+  uint32_t slot, chan, msg, msg_gen;
+  uint32_t offset, bitlen, level_size;
   Clock::time_point seen;
 };
 
@@ -172,7 +179,7 @@ struct hg_service {
   std::deque<Pending> pending;
   struct LaneState {
     bool busy = false;
-    std::vector<uint32_t> slots;
+    std::vector<Pending> slots;
   };
   std::vector<LaneState> lanes;
   int busy = 0;
@@ -183,14 +190,25 @@ struct hg_service {
   uint64_t max_in_flight = 0;
   Clock::time_point last_arrival;
   // requests released by finished batches whose clients have not submitted
-  // again (cfg.follow): a closed-loop cohort is back when this reaches zero
+  // again (cfg.follow): a closed-loop cohort is back when this reaches zero.
+  // Counted per channel, so that only a resubmission from a channel whose
+  // requests were released counts (open-loop arrivals from other channels do
+  // not make the cohort look complete)
   uint64_t returning = 0;
+  std::vector<uint32_t> released;  // per channel
   bool released_any = false;
-  std::vector<uint32_t> take;
+  std::vector<Pending> take;
+  // channels whose handle closed with requests in flight (kChanOrphaned):
+  // adopted[ch] once the dispatcher has swept the ring the handle left
+  std::vector<uint8_t> adopted;
+  uint32_t seen_orphans = 0;
 
   bool intake();
   void complete(int lane, const int32_t* codes, int32_t fail);
-  void finish_slots(const uint32_t* ids, size_t n, const int32_t* codes, int32_t fail);
+  void finish_slots(const Pending* items, size_t n, const int32_t* codes, int32_t fail);
+  void free_slot(uint32_t id, uint32_t ch);
+  void adopt(uint32_t ch);
+  void sweep_orphans();
   void drain();
   void launch(int lane);
   void run();
@@ -211,8 +229,12 @@ bool hg_service::intake() {
       Slot* s = v.slot(id);
       if (s->state.load(std::memory_order_acquire) != kSlotQueued) continue;
       s->state.store(kSlotTaken, std::memory_order_relaxed);
-      pending.push_back(Pending{id, s->msg, s->msg_gen, now});
-      if (returning) returning--;
+      Pending p{id, s->chan, s->msg, s->msg_gen, s->offset, s->bitlen, s->level_size, now};
+      pending.push_back(p);
+      if (p.chan < released.size() && released[p.chan]) {
+        released[p.chan]--;
+        if (returning) returning--;
+      }
       any = true;
     }
   }
@@ -220,17 +242,64 @@ bool hg_service::intake() {
   return any;
 }
 
-// codes into the slots, slot ids into their channels' rings, one wake per channel
-void hg_service::finish_slots(const uint32_t* ids, size_t n, const int32_t* codes, int32_t fail) {
+// a finished slot of an orphaned channel: nobody will collect it, so the
+// dispatcher frees it; the channel is released once it owns no slot
+void hg_service::free_slot(uint32_t id, uint32_t ch) {
+  Slot* s = v.slot(id);
+  s->state.store(kSlotFree, std::memory_order_release);
+  v.free_bits()[id / 64].fetch_or(1ull << (id % 64), std::memory_order_release);
+  Channel* c = v.chan(ch);
+  if (c->inflight.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+    adopted[ch] = 0;
+    c->used.store(kChanFree, std::memory_order_release);
+  }
+}
+
+// takes over an orphaned channel: the completions pushed after its handle's
+// last drain (ring positions [head, tail)) are freed here
+void hg_service::adopt(uint32_t ch) {
+  Channel* c = v.chan(ch);
+  adopted[ch] = 1;
+  const uint32_t cap = v.h->nslots;
+  const uint32_t* ring = v.ring(ch);
+  std::vector<uint32_t> ids;
+  for (uint32_t k = c->head; k != tails[ch]; k++) ids.push_back(ring[k % cap]);
+  for (uint32_t id : ids)
+    if (id < cap && v.slot(id)->state.load(std::memory_order_acquire) == kSlotDone) free_slot(id, ch);
+  if (adopted[ch] && c->inflight.load(std::memory_order_acquire) == 0) {
+    adopted[ch] = 0;
+    c->used.store(kChanFree, std::memory_order_release);
+  }
+}
+
+void hg_service::sweep_orphans() {
+  const uint32_t o = v.h->orphans.load(std::memory_order_acquire);
+  if (o == seen_orphans) return;
+  seen_orphans = o;
+  for (uint32_t ch = 0; ch < v.h->nchan; ch++)
+    if (!adopted[ch] && v.chan(ch)->used.load(std::memory_order_acquire) == kChanOrphaned) adopt(ch);
+}
+
+// codes into the slots, slot ids into their channels' rings, one wake per
+// channel (the channel is the one intake() recorded, not the slot's word now)
+void hg_service::finish_slots(const Pending* items, size_t n, const int32_t* codes, int32_t fail) {
   if (n == 0) return;
   const uint32_t cap = v.h->nslots;
   for (size_t i = 0; i < n; i++) {
-    Slot* s = v.slot(ids[i]);
-    const uint32_t ch = s->chan;
+    const uint32_t id = items[i].slot, ch = items[i].chan;
+    Slot* s = v.slot(id);
     s->code = codes ? codes[i] : fail;
     s->state.store(kSlotDone, std::memory_order_release);
     if (ch >= v.h->nchan) continue;
-    v.ring(ch)[tails[ch] % cap] = ids[i];
+    Channel* c = v.chan(ch);
+    if (c->used.load(std::memory_order_acquire) == kChanOrphaned) {
+      if (!adopted[ch]) adopt(ch);
+      if (adopted[ch]) {
+        free_slot(id, ch);
+        continue;
+      }
+    }
+    v.ring(ch)[tails[ch] % cap] = id;
     tails[ch]++;
     touched[ch] = 1;
   }
@@ -246,6 +315,8 @@ void hg_service::finish_slots(const uint32_t* ids, size_t n, const int32_t* code
 void hg_service::complete(int lane, const int32_t* codes, int32_t fail) {
   LaneState& L = lanes[lane];
   finish_slots(L.slots.data(), L.slots.size(), codes, fail);
+  for (const Pending& p : L.slots)
+    if (p.chan < released.size()) released[p.chan]++;
   returning += L.slots.size();
   released_any = true;
   v.h->batches.fetch_add(1, std::memory_order_relaxed);
@@ -275,10 +346,9 @@ void hg_service::launch(int lane) {
   const bool msg_ok = first.msg < kMaxMsgs && m.gen == first.msg_gen &&
                       m.state.load(std::memory_order_acquire) == kMsgReady && m.len <= kMsgCap;
   if (!msg_ok) {  // a stale message reference: fail that request alone
-    const uint32_t id = first.slot;
     pending.pop_front();
     const int32_t code = HG_ERR_ARG;
-    finish_slots(&id, 1, &code, 0);
+    finish_slots(&first, 1, &code, 0);
     return;
   }
   if ((int)first.msg != cur_msg || first.msg_gen != cur_gen) {
@@ -291,10 +361,10 @@ void hg_service::launch(int lane) {
     if (rc != HG_OK && rc != HG_ERR_HASH_EOF) {
       fprintf(stderr, "hg_service: message setup failed (%d)\n", rc);
       cur_msg = -1;
-      std::vector<uint32_t> ids;
+      std::vector<Pending> ids;
       for (auto it = pending.begin(); it != pending.end();) {
         if (it->msg == first.msg && it->msg_gen == first.msg_gen) {
-          ids.push_back(it->slot);
+          ids.push_back(*it);
           it = pending.erase(it);
         } else {
           ++it;
@@ -308,17 +378,16 @@ void hg_service::launch(int lane) {
   take.clear();
   size_t nwords = 0;
   const uint32_t max_bits = v.h->slot_words * 64;
-  std::vector<uint32_t> bad;
+  std::vector<Pending> bad;
   for (auto it = pending.begin(); it != pending.end() && take.size() < cfg.max_batch;) {
     if (it->msg != first.msg || it->msg_gen != first.msg_gen) {
       ++it;
       continue;
     }
-    const Slot* s = v.slot(it->slot);
-    if (s->bitlen > max_bits) bad.push_back(it->slot);
+    if (it->bitlen > max_bits) bad.push_back(*it);
     else {
-      take.push_back(it->slot);
-      nwords += (s->bitlen + 63) / 64;
+      take.push_back(*it);
+      nwords += (it->bitlen + 63) / 64;
     }
     it = pending.erase(it);
   }
@@ -344,9 +413,10 @@ void hg_service::launch(int lane) {
   if (rc == HG_OK) {
     uint32_t wo = 0;
     for (size_t i = 0; i < take.size(); i++) {
-      Slot* s = v.slot(take[i]);
-      const uint32_t nw = (s->bitlen + 63) / 64;
-      r[i] = hg_request{s->offset, s->bitlen, s->level_size, wo};
+      const Pending& p = take[i];
+      Slot* s = v.slot(p.slot);
+      const uint32_t nw = (p.bitlen + 63) / 64;  // <= slot_words: checked above on the same copy
+      r[i] = hg_request{p.offset, p.bitlen, p.level_size, wo};
       memcpy(sg + 64 * i, s->sig, 64);
       memcpy(w + wo, s->words(), 8ull * nw);
       wo += nw;
@@ -376,6 +446,7 @@ void hg_service::run() {
       progress = true;
     }
     progress |= intake();
+    sweep_orphans();
     const bool stopping = stop.load(std::memory_order_acquire);
     while (!pending.empty()) {
       int free_lane = -1;
@@ -405,6 +476,7 @@ void hg_service::run() {
     bool queued = false;
     std::atomic<uint64_t>* qb = v.queued_bits();
     for (uint32_t w = 0; w < h->nslots / 64 && !queued; w++) queued = qb[w].load(std::memory_order_seq_cst) != 0;
+    queued = queued || h->orphans.load(std::memory_order_seq_cst) != seen_orphans;
     if (!queued && !stop.load(std::memory_order_acquire)) futex_wait(&h->doorbell, bell, 20000);
     h->sleeping.store(0, std::memory_order_seq_cst);
   }
@@ -466,6 +538,8 @@ int create_common(const char* name, const hg_service_config* in, uint32_t nreg, 
   for (uint32_t w = 0; w < cfg.slots / 64; w++) fb[w].store(~0ull, std::memory_order_relaxed);
   s->tails.assign(cfg.channels, 0);
   s->touched.assign(cfg.channels, 0);
+  s->released.assign(cfg.channels, 0);
+  s->adopted.assign(cfg.channels, 0);
   s->lanes.resize(cfg.lanes);
   return HG_OK;
 }
@@ -551,8 +625,7 @@ void hg_service_destroy(hg_service* s) {
   // requests queued after the last look fail; every sleeper wakes and sees kStopped
   s->pending.clear();
   (void)s->intake();
-  std::vector<uint32_t> ids;
-  for (const Pending& p : s->pending) ids.push_back(p.slot);
+  std::vector<Pending> ids(s->pending.begin(), s->pending.end());
   s->finish_slots(ids.data(), ids.size(), nullptr, HG_ERR_DEVICE);
   for (uint32_t c = 0; c < h->nchan; c++) {
     s->v.chan(c)->tail.fetch_add(0, std::memory_order_seq_cst);

@@ -34,13 +34,17 @@
 namespace hgshm {
 
 constexpr uint64_t kMagic = 0x3130435653474855ull;  // "UHGSVC01"
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;
 constexpr uint32_t kMaxMsgs = 32;   // distinct messages pinned at once
 constexpr uint32_t kMsgCap = 1024;  // bytes of one message
 
 enum : uint32_t { kSlotFree = 0, kSlotFilling = 1, kSlotQueued = 2, kSlotTaken = 3, kSlotDone = 4 };
 enum : uint32_t { kRunning = 1, kStopping = 2, kStopped = 3 };
 enum : uint32_t { kMsgEmpty = 0, kMsgBusy = 1, kMsgReady = 2 };
+// Channel.used: free, held by a client handle, or orphaned (its handle closed
+// with requests in flight: the service frees those slots itself and releases
+// the channel once none is left, so no later handle sees foreign completions)
+enum : uint32_t { kChanFree = 0, kChanUsed = 1, kChanOrphaned = 2 };
 
 static_assert(sizeof(std::atomic<uint32_t>) == 4 && sizeof(std::atomic<uint64_t>) == 8, "lock-free shared words");
 
@@ -59,11 +63,14 @@ struct alignas(64) Slot {
 static_assert(sizeof(Slot) == 128, "slot header");
 
 struct alignas(64) Channel {
-  std::atomic<uint32_t> used;     // claimed by a client handle
-  std::atomic<uint32_t> tail;     // completions pushed so far (futex word)
-  std::atomic<uint32_t> waiters;  // client threads asleep on tail
+  std::atomic<uint32_t> used;      // kChanFree / kChanUsed / kChanOrphaned
+  std::atomic<uint32_t> tail;      // completions pushed so far (futex word)
+  std::atomic<uint32_t> waiters;   // client threads asleep on tail
   uint32_t pid;
+  std::atomic<uint32_t> inflight;  // slots of this channel claimed and not yet freed
+  uint32_t head;                   // the closing handle's ring position (valid once orphaned)
 };
+static_assert(sizeof(Channel) == 64, "channel");
 
 struct alignas(64) Msg {
   std::atomic<uint32_t> state;  // kMsgEmpty / kMsgBusy (being written) / kMsgReady
@@ -83,6 +90,7 @@ struct alignas(64) Header {
   std::atomic<uint32_t> sleeping;
   alignas(64) std::atomic<uint32_t> msg_lock;  // guards msgs[] rewrites (rare)
   alignas(64) std::atomic<uint64_t> batches, requests;
+  std::atomic<uint32_t> orphans;  // bumped by every handle closed with requests in flight
   Msg msgs[kMaxMsgs];
 };
 

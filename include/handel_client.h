@@ -29,7 +29,11 @@ typedef struct hg_client hg_client;
 /* Attaches to the service region `name`; HG_ERR_ARG if it does not exist,
  * is not a running service, or has no free channel. */
 int hg_client_open(const char* name, hg_client** out);
-/* Releases the handle (tickets not yet collected are dropped). */
+/* Releases the handle (tickets not yet collected are dropped: the service
+ * frees their slots when they finish, and keeps the handle's channel reserved
+ * until then, so no later handle receives their completions). Must not run
+ * concurrently with submit / wait / wait_any on the same handle: stop the
+ * threads that use it first. */
 void hg_client_close(hg_client* cl);
 /* Queues one processing.go verifySignature (:342-368): the level range
  * [req->offset, req->offset + req->level_size), the bitset of req->bitlen bits

@@ -233,3 +233,149 @@ def test_verifierd_rejects_bad_arguments(tmp_path):
     bad.write_bytes(bytes(100))  # not a multiple of 128
     r = subprocess.run([exe, "--name", service_name("vd2"), "--registry", str(bad)], capture_output=True, text=True)
     assert r.returncode == 2 and "128-byte" in r.stderr
+
+
+def _slot_view(name):
+    """The service region mapped into this process (the layout of hg_shm.h):
+    (mmap, slot byte offset fn, slot_words). Test-only: a misbehaving client."""
+    import mmap
+    import struct
+
+    fd = os.open("/dev/shm" + name, os.O_RDWR)
+    try:
+        size = os.fstat(fd).st_size
+        m = mmap.mmap(fd, size)
+    finally:
+        os.close(fd)
+    nslots, slot_words = struct.unpack_from("<II", m, 12)
+    stride, off_slots = struct.unpack_from("<QQ", m, 32)
+    return m, (lambda i: off_slots + stride * i), slot_words
+
+
+@pytest.mark.parametrize("new_bitlen", ["max", "huge"])
+def test_client_rewriting_its_queued_slot_cannot_change_the_batch(new_bitlen):
+    """The service copies a slot's header once when it takes the slot: a client
+    that rewrites bitlen / level_size / offset after queuing gets the verdict
+    of what it queued (the snapshot), never a different sizing of the copy
+    into the GPU staging buffer (launch used to re-read bitlen)."""
+    import struct
+    import time
+
+    name = service_name("echo7")
+    # one lane, a long linger and no follow policy: the request sits in the
+    # dispatcher's pending queue (already taken) while the client rewrites it
+    with EchoService(name, nreg=256, delay_us=10, lanes=1, max_wait_us=300_000, follow=0) as svc, \
+            Client(name) as cl:
+        m, slot_at, slot_words = _slot_view(name)
+        try:
+            w = np.array([0x1234_5678_9abc_def0], dtype=np.uint64)
+            t = cl.submit(MSG, 64, 64, 64, w, echo_signature(w))
+            t_bad = cl.submit(MSG, 64, 64, 64, w, echo_signature(w, True))
+            time.sleep(0.05)  # taken by the dispatcher, not launched (300 ms linger)
+            big = slot_words * 64 if new_bitlen == "max" else 0xFFFFFFFF
+            for tk in (t, t_bad):
+                base = slot_at(tk & 0xFFFFFFFF)
+                state = struct.unpack_from("<I", m, base)[0]
+                assert state == 3, "the slot is Taken (kSlotTaken) while it lingers"
+                struct.pack_into("<III", m, base + 24, 0, big, big)  # offset, bitlen, level_size
+            assert cl.wait(t) == 0
+            assert cl.wait(t_bad) == _lib.HG_ERR_SIG_INVALID
+            assert svc.stats()[1] == 2
+        finally:
+            m.close()
+
+
+def test_close_with_tickets_in_flight_keeps_the_channel_until_they_finish():
+    """hg_client_close with requests still queued: their slots
+    come back to the free pool, the channel is reserved until then, and the
+    next handle on it only ever sees its own tickets."""
+    import time
+
+    name = service_name("echo8")
+    with EchoService(name, nreg=128, delay_us=150_000, lanes=1, channels=1, slots=64, max_wait_us=10):
+        a = Client(name)
+        w = np.ones(1, dtype=np.uint64)
+        for _ in range(10):
+            a.submit(MSG, 0, 64, 64, w, echo_signature(w))
+        a.close()  # ten tickets in flight
+        from handel_amd._lib import HandelGPUError
+        with pytest.raises(HandelGPUError):
+            Client(name)  # the one channel stays reserved while they run
+        t0 = time.time()
+        b = None
+        while b is None:
+            try:
+                b = Client(name)
+            except HandelGPUError:
+                assert time.time() - t0 < 5, "the orphaned channel was never released"
+                time.sleep(0.01)
+        with b:
+            # every slot is free again: the whole region can be claimed at once
+            mine = {b.submit(MSG, 0, 64, 64, w, echo_signature(w, i % 2 == 1)): (i % 2) for i in range(64)}
+            got = {}
+            while len(got) < len(mine):
+                for tk, c in b.wait_any(cap=64, timeout_us=2_000_000):
+                    assert tk in mine and tk not in got, "a ticket this handle never issued"
+                    got[tk] = c
+            assert got == mine
+
+
+def test_close_after_completion_releases_the_channel_at_once():
+    name = service_name("echo9")
+    with EchoService(name, nreg=128, delay_us=10, lanes=1, channels=1, slots=64):
+        a = Client(name)
+        w = np.ones(1, dtype=np.uint64)
+        tk = [a.submit(MSG, 0, 64, 64, w, echo_signature(w)) for _ in range(64)]
+        assert a.wait(tk[0]) == 0
+        import time
+        time.sleep(0.05)  # the rest finish; never collected
+        a.close()
+        with Client(name) as b:  # no wait: close freed every finished slot
+            assert b.verify(MSG, 0, 64, 64, w, echo_signature(w)) == 0
+
+
+def test_follow_policy_counts_only_returning_channels():
+    """follow=1 launches when the finished batches' cohort has resubmitted; an
+    arrival on a channel that had nothing released must not count as a
+    returning request, so a lone open-loop request still waits
+    for max_wait_us to batch with others."""
+    import time
+
+    name = service_name("echo10")
+    with EchoService(name, nreg=128, delay_us=10, lanes=2, max_wait_us=200_000, follow=1) as svc, \
+            Client(name) as a, Client(name) as b:
+        w = np.ones(1, dtype=np.uint64)
+        # a: one closed-loop round (its batch leaves after the 200 ms linger)
+        assert a.verify(MSG, 0, 64, 64, w, echo_signature(w)) == 0
+        # b (nothing released to it) submits twice, 20 ms apart: both ride one batch
+        tb = [b.submit(MSG, 0, 64, 64, w, echo_signature(w))]
+        time.sleep(0.02)
+        tb.append(b.submit(MSG, 0, 64, 64, w, echo_signature(w)))
+        assert [b.wait(t) for t in tb] == [0, 0]
+        assert svc.stats()[0] == 2, svc.stats()
+
+
+def test_service_trust_boundary_under_asan(tmp_path):
+    """tests/native/service_asan.cpp: the service and client sources built for
+    the CPU with AddressSanitizer + UBSan (no HIP: the echo executor) and run
+    through three scenarios — slot headers rewritten after queuing, a handle
+    closed with tickets in flight, a thread rewriting random slots' size
+    fields under load. Any out-of-bounds access aborts the run."""
+    import shutil
+
+    gxx = shutil.which("g++")
+    if not gxx:
+        pytest.skip("no g++")
+    root = os.path.join(os.path.dirname(__file__), "..")
+    exe = str(tmp_path / "service_asan")
+    srcs = [os.path.join(root, "handel_amd", "csrc", "hg_service.cpp"),
+            os.path.join(root, "handel_amd", "csrc", "hg_client.cpp"),
+            os.path.join(root, "tests", "native", "service_asan.cpp")]
+    subprocess.run([gxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    *srcs, "-lpthread", "-o", exe], check=True, capture_output=True, timeout=300)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1]) == {"failures": 0}
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
