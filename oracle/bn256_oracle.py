@@ -932,6 +932,11 @@ def verify_request(registry_pks: Sequence, lo: int, hi: int, bits: Sequence[bool
         return ERR_LEVEL
     status, agg = aggregate_pk(ids, bits)
     if status == "nil":
+        # VerifySignature hashes the message before it pairs the nil aggregate
+        # (bn256/go/bn256.go:84-88): an unhashable message is reported first
+        _, herr = hashed_message(msg)
+        if herr is not None:
+            return "handel: " + herr
         return ERR_EMPTY_AGGREGATE
     err = (verify_signature_fast if fast else verify_signature)(agg, msg, sig)
     if err is not None:

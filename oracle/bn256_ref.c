@@ -1362,7 +1362,12 @@ long ref_verify_batch(const uint8_t* msg, size_t msglen, const uint8_t* pks, con
  * request r covers registry[off[r], off[r]+bitlen[r]) with its bitset words
  * at words + woff[r] (willf layout), signature sigs + 64r. level_len[r] is the
  * partitioner's level size; bitlen != level_len -> RC_LEVEL. agg_out (nullable)
- * receives the 128-byte marshal of the aggregate key. */
+ * receives the 128-byte marshal of the aggregate key.
+ * Precedence when several errors apply (the order the reference meets them):
+ * the signature's unmarshal (Handel.parseSignatures -> MultiSignature.Unmarshal,
+ * handel.go:390-395) before the bit length (handel.go:399-402,
+ * processing.go:350-352); in VerifySignature hashedMessage (bn256/go/bn256.go:
+ * 84-88) before the pairing of a nil aggregate (RC_EMPTY_AGG). */
 typedef struct {
   const uint8_t* reg;
   size_t nreg;
@@ -1381,7 +1386,13 @@ static void* agg_worker(void* arg) {
   ajob* j = (ajob*)arg;
   for (size_t r = j->begin; r < j->end; r++) {
     uint32_t bl = j->bitlen[r];
-    if (bl != j->level_len[r] || (size_t)j->off[r] + bl > j->nreg) { j->codes[r] = RC_LEVEL; continue; }
+    fp sx, sy;
+    int sinf;
+    const int sig_bad = dec_g1(j->sigs + 64 * r, 64, FLAVOR_GO, &sx, &sy, &sinf) != RC_OK;
+    if (bl != j->level_len[r] || (size_t)j->off[r] + bl > j->nreg) {
+      j->codes[r] = sig_bad ? RC_SIG_UNMARSHAL : RC_LEVEL;
+      continue;
+    }
     g2j acc;
     g2_set_inf(&acc);
     int any = 0, bad = 0;
@@ -1397,12 +1408,10 @@ static void* agg_worker(void* arg) {
       g2_add(&acc, &acc, &pt);
       any = 1;
     }
-    if (bad) { j->codes[r] = RC_PK_UNMARSHAL; continue; }
+    if (bad) { j->codes[r] = sig_bad ? RC_SIG_UNMARSHAL : RC_PK_UNMARSHAL; continue; }
     if (j->agg_out) enc_g2(j->agg_out + 128 * r, &acc);
+    if (sig_bad) { j->codes[r] = RC_SIG_UNMARSHAL; continue; }
     if (!any) { j->codes[r] = RC_EMPTY_AGG; continue; }
-    fp sx, sy;
-    int sinf;
-    if (dec_g1(j->sigs + 64 * r, 64, FLAVOR_GO, &sx, &sy, &sinf)) { j->codes[r] = RC_SIG_UNMARSHAL; continue; }
     fp2 qx = F2_ZERO, qy = F2_ZERO;
     int pinf = g2_is_inf(&acc);
     if (!pinf) g2_affine(&qx, &qy, &acc);
@@ -1440,6 +1449,7 @@ long ref_verify_aggregate(const uint8_t* msg, size_t msglen, const uint8_t* reg,
   for (size_t r = 0; r < nreq; r++) {
     if (!hash_ok && codes[r] == RC_OK) codes[r] = RC_HASH_EOF;
     if (!hash_ok && codes[r] == RC_SIG_INVALID) codes[r] = RC_HASH_EOF;
+    if (!hash_ok && codes[r] == RC_EMPTY_AGG) codes[r] = RC_HASH_EOF;
     ok += codes[r] == RC_OK;
   }
   return ok;

@@ -328,3 +328,44 @@ def test_aggregate_c_matches_python():
         assert agg_b[128 * j:128 * j + 128] == O.g2_marshal(agg)
         assert O.verify_request(pks, off, off + size, bits, O.g1_unmarshal(sigs[64 * j:64 * j + 64])[0],
                                 msg) is None
+
+
+def test_aggregate_error_precedence_follows_the_reference_flow():
+    """When several errors apply to one request, the oracle reports the one
+    the reference meets first: the signature's unmarshal in
+    Handel.parseSignatures (handel.go:390-395) before the bit length
+    (handel.go:399-402, processing.go:350-352); hashedMessage inside
+    VerifySignature (bn256/go/bn256.go:84-88) before the nil aggregate's
+    pairing (the panic, HG_ERR_EMPTY_AGG)."""
+    import numpy as np
+
+    from oracle import bn256_oracle as O
+    from oracle import ref_lib as R
+    from tests import _fixtures as F
+
+    ks, reg, _ = F.keys_and_sigs(8, seed=b"precedence")
+    good = R.sign(F.LIB_MESSAGE, F.scalar_bytes(ks[:1]))
+    bad = b"\xff" * 32 + good[32:]  # x >= p: no point
+    #            (off, bitlen, level, word)  words
+    cases = [((0, 8, 8, 0), 0xFF, bad, 5),    # bad signature only
+             ((0, 7, 8, 0), 0x7F, bad, 5),    # bad signature + bit length off its level
+             ((0, 8, 8, 0), 0x00, bad, 5),    # bad signature + empty bitset
+             ((0, 7, 8, 0), 0x00, good, 3),   # level + empty
+             ((0, 8, 8, 0), 0x00, good, 6),   # empty only
+             ((0, 1, 1, 0), 0x01, good, 0)]   # key 0's own signature
+    reqs = [c[0] for c in cases]
+    words = np.array([c[1] for c in cases], dtype=np.uint64)
+    woff = np.arange(len(cases), dtype=np.uint64)
+    sigs = b"".join(c[2] for c in cases)
+    got = R.verify_aggregate(F.LIB_MESSAGE, reg, [r[0] for r in reqs], [r[1] for r in reqs], [r[2] for r in reqs],
+                             words, woff, sigs, nthreads=1)
+    assert got.tolist() == [c[3] for c in cases]
+    # an unhashable message: EOF before the nil aggregate, the level error first
+    msg = F.REJECT_MESSAGES[0]
+    assert O.hash_scalar(msg)[1] is not None
+    got = R.verify_aggregate(msg, reg, [r[0] for r in reqs], [r[1] for r in reqs], [r[2] for r in reqs],
+                             words, woff, sigs, nthreads=1)
+    assert got.tolist() == [5, 5, 5, 3, 2, 2]
+    pks = [O.g2_unmarshal(reg[128 * i:128 * i + 128], "go")[0] for i in range(8)]
+    assert O.verify_request(pks, 0, 8, [False] * 8, O.G1_GEN, msg) == "handel: EOF"
+    assert O.verify_request(pks, 0, 8, [False] * 8, O.G1_GEN, F.LIB_MESSAGE) == O.ERR_EMPTY_AGGREGATE
