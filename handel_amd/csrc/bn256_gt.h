@@ -73,6 +73,14 @@ void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt
 // the kernel), then fe[r] == y[r] where still HG_OK
 void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s,
                         bool pad = true);
+// launch_sig_pairing on five 12-lane teams per wave (bn256_sig12.hip): the
+// lines evaluated at -sig first (k_sig_lines, into ev: sig12_lines_bytes(n)),
+// then k_verify_sig12; the same fe values
+size_t sig12_lines_bytes(int n);
+void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Fp* ev, Gt* fe,
+                          hipStream_t s, bool pad);
+// the 12-lane kernel is the default; HG_SIG12=0 selects launch_sig_pairing
+bool sig12_enabled();
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s);
 // the same, and the verdict bitset (ceil(n / 8) bytes, hg_pack_verdicts_device's layout)
 void launch_gt_compare_bits(const Gt* fe, const Gt* y, int n, int32_t* codes, uint8_t* bits, hipStream_t s);

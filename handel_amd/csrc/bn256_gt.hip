@@ -34,6 +34,7 @@
 #include "bn256_gt.h"
 #include "bn256_k6.h"
 #include "bn256_pairing.h"
+#include "bn256_sigfe.h"
 
 namespace hg {
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
@@ -773,66 +774,6 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
   ILfix::run(T, S, after);
 }
 
-// team_final_exp_fc (bn256_pairing.h) on layout S: the same chain over seven
-// slots F, A, B, C, D, E, G (the full layout spreads it over eleven), so the
-// team region is 118 elements instead of 180: eight pairing waves and a fold
-// workgroup fit in a CU's LDS. Slot roles: F = res; the easy part's inversion
-// uses D, E; the exponentiations by v ping-pong D <-> E with the base's
-// conjugate in G; t0 = A, t1 = B, t2 = C, t4 = G, t3 = B (once t1 is
-// consumed); D carries the Frobenius temporaries of the last products. The
-// next base t2^2 is a product, not the canonical cyclotomic squaring, whose
-// pre-pass scratch would end the region 2 elements later.
-HG_DEV constexpr XHint final_exp_hint_s() { return xh<IMul12S<S_E, S_F, S_D>>(); }
-HG_DEV void team_final_exp_fc_s(const Team& T, XStream& S) {
-  // easy part: res = f^((p^6 - 1)(p^2 + 1)), f^-1 = conj(f) / (f conj(f))
-  t12_conj(T, S_D, S_F);
-  IMul12S<S_E, S_F, S_D>::run(T, S, xh<IMul12S<S_A, S_D, S_E>>());  // N = f conj(f)
-  t12_inv_norm(T, S_E);                                              // N^-1
-  IMul12S<S_A, S_D, S_E>::run(T, S, xh<IMul12S<S_F, S_B, S_A>>());  // A = f^-1
-  t12_conj(T, S_B, S_F);
-  IMul12S<S_F, S_B, S_A>::run(T, S, xh<IMul12S<S_F, S_F, S_A>>());  // f^(p^6 - 1)
-  t12_frob2(T, S_A, S_F);
-  IMul12S<S_F, S_F, S_A>::run(T, S, xh<ICycS<S_E, S_D>>());         // res
-  t12_copy(T, S_D, S_F);  // base of the first exponentiation
-#pragma unroll 1
-  for (int ph = 0; ph < 3; ph++) {
-#pragma unroll 1
-    for (int st = 0; st < 3; st++) {  // E = D^v, D = E^v, E = D^v
-      const XHint next = st < 2 ? ((st & 1) ? xh<ICycS<S_E, S_D>>() : xh<ICycS<S_D, S_E>>())
-                                : (ph == 0 ? xh<ICycS<S_A, S_A>>() : ph == 1 ? xh<IMul12S<S_B, S_C, S_G>>()
-                                                                             : xh<IMul12S<S_G, S_B, S_E>>());
-      if ((st & 1) == 0) t12_pow_v_s<S_E, S_D, S_G>(T, S, next);
-      else t12_pow_v_s<S_D, S_E, S_G>(T, S, next);
-    }
-    if (ph == 0) {  // t0 = conj(res^u)^2, t1 = t0^2 t0; next base t1
-      t12_conj(T, S_A, S_E);
-      ICycS<S_A, S_A>::run(T, S, xh<ICycS<S_B, S_A>>());
-      ICycS<S_B, S_A>::run(T, S, xh<IMul12S<S_B, S_A, S_B>>());
-      IMul12S<S_B, S_A, S_B>::run(T, S, xh<ICycS<S_E, S_D>>());
-      t12_copy(T, S_D, S_B);
-    } else if (ph == 1) {  // t2 = conj(t1^u), t1 = t2 conj(t1); next base t3 = t2^2
-      t12_conj(T, S_C, S_E);
-      t12_conj(T, S_G, S_B);
-      IMul12S<S_B, S_C, S_G>::run(T, S, xh<IMul12S<S_D, S_C, S_C>>());
-      IMul12S<S_D, S_C, S_C>::run(T, S, xh<ICycS<S_E, S_D>>());  // canonical (feeds a conj)
-    } else {  // t4 = t1 t3^u
-      IMul12S<S_G, S_B, S_E>::run(T, S, xh<IMul12S<S_B, S_A, S_G>>());
-    }
-  }
-  IMul12S<S_B, S_A, S_G>::run(T, S, xh<IMul12S<S_A, S_C, S_G>>());  // t3 = t0 t4
-  IMul12S<S_A, S_C, S_G>::run(T, S, xh<IMul12S<S_A, S_F, S_A>>());  // t0 = t2 t4
-  IMul12S<S_A, S_F, S_A>::run(T, S, xh<IMul12S<S_A, S_D, S_A>>());  // t0 = res t0
-  t12_frob(T, S_D, S_B);
-  IMul12S<S_A, S_D, S_A>::run(T, S, xh<IMul12S<S_A, S_D, S_A>>());  // t0 = frob(t3) t0
-  t12_frob2(T, S_D, S_G);
-  IMul12S<S_A, S_D, S_A>::run(T, S, xh<IMul12S<S_D, S_D, S_B>>());  // t0 = frob2(t4) t0
-  t12_conj(T, S_D, S_F);
-  IMul12S<S_D, S_D, S_B>::run(T, S, xh<IMul12S<S_F, S_D, S_A>>());  // t2 = conj(res) t3
-  t12_frob(T, S_D, S_D);
-  t12_frob2(T, S_D, S_D);                                            // t2 = frob^3(t2)
-  IMul12S<S_F, S_D, S_A>::run(T, S, xh_none());                      // result
-}
-
 // true (team-uniform) when slots a and b hold the same value (both canonical)
 HG_DEV bool t12_equal(const Team& T, int a, int b) {
   Fp u, v;
@@ -883,8 +824,8 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
   if (kStore) (void)decode_g1_one(sig_bytes + (size_t)ci * 64, flavor, sg);
   else sg = sigs[ci];
   XStream S = x_stream();
-  team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, final_exp_hint_s());
-  team_final_exp_fc_s(T, S);
+  team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, SigFE<SigProgs16>::final_exp_hint_s());
+  SigFE<SigProgs16>::team_final_exp_fc_s(T, S);
   if (kStore) {
     team_sync();
     if (valid) gt_store(T, S_F, fe + idx);

@@ -1,0 +1,216 @@
+// bn256_sig12.hip — the GT path's signature-side pairing on FIVE 12-lane teams
+// per wave (k_verify_sig12), with the G2Base lines evaluated ahead
+// (k_sig_lines).
+//
+// The check (processing.go:342-368 -> bn256/go/bn256.go:82-94, GT form in
+// bn256_gt.hip) needs per signature FE(Miller(G2Base at -sig)). k_verify_sig
+// runs it on 16-lane teams: lanes 0..11 own the twelve Fp coefficients of f,
+// lanes 12..15 evaluate the next G2Base line at -sig beside f^2 — and idle
+// through the final exponentiation, which is ~60 % of the kernel. Here the
+// 85 line evaluations of every signature (b' = bx * x_sig, c' = cy * -y_sig:
+// four Fp products per line, bn256_gt.hip team_miller_sig) run first, as
+// their own wide kernel, into HBM; the pairing kernel then needs only lanes
+// 0..11 of a team, and a wave carries five checks instead of four: 20 % fewer
+// wave-instructions per batch for the same per-wave program (the team
+// programs are the generator's 12-lane forms: every pre-pass value on lanes
+// 0..11, tools/gen_g2_schedule.py PRE_LANES).
+//
+// Evaluated lines in HBM: ev[(s * n + c) * 4 + j], j = FB.x, FB.y, FC.x, FC.y
+// of line s for check c (160 bytes; a wave's five teams read 800 contiguous
+// bytes per line). 85 lines x 160 B = 13.6 KB per check. k_sig_scalars
+// decodes each signature once, k_sig_lines runs one product per thread (n x
+// 340 threads: the whole GPU, a few microseconds per batch).
+//
+// Team region (layout T, tools/gen_g2_schedule.py): five Fp12 slots and the
+// register file, 94 elements — the final exponentiation parks two of its
+// seven live values in HBM (bn256_sigfe.h team_final_exp_fc_t) — so a wave of
+// five teams takes 18.8 KB of LDS and a CU holds eight pairing waves (two
+// per SIMD: the unpadded kernel's 247 VGPRs allow it) beside a fold
+// workgroup.
+//
+// Values are identical to k_verify_sig's (the same Montgomery products in the
+// same order, canonical), so the FE values, and every verdict, are too.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "bn256_decode.h"
+#include "bn256_g2sched.h"
+#include "bn256_gt.h"
+#include "bn256_sigfe.h"
+
+namespace hg {
+
+// the signature's evaluation scalars: sc[2c] = x_sig, sc[2c + 1] = -y_sig
+// (both 0 at infinity: e(inf, G2Base) = 1, every line evaluates to w^3, which
+// the final exponentiation maps to 1 — bn256_gt.hip team_miller_sig). A
+// signature that fails to decode gives meaningless lines: its FE value is
+// never compared (its code is the decode error, k_agg_prologue).
+__global__ __launch_bounds__(256) void k_sig_scalars(const uint8_t* sig_bytes, int flavor, int n, Fp* sc) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n) return;
+  PointG1 sg;
+  (void)decode_g1_one(sig_bytes + (size_t)c * 64, flavor, sg);
+  Fp nsy, z;
+  fp_zero(z);
+  fp_neg(nsy, sg.y);
+  const bool use = sg.inf == 0;
+  fp_sel(sc[2 * c], use, sg.x, z);
+  fp_sel(sc[2 * c + 1], use, nsy, z);
+}
+
+// ev[(s * n + c) * 4 + j] = component j of line s at -sig_c: one Montgomery
+// product per thread (FB = bx * x_sig, FC = cy * -y_sig), consecutive threads
+// on consecutive 40-byte results
+__global__ __launch_bounds__(256) void k_sig_lines(const Fp* sc, int n, const LineCoef* tab, Fp* ev) {
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (size_t)n * kNumLines * 4) return;
+  const int j = (int)(t & 3);
+  const size_t q = t >> 2;
+  const int c = (int)(q % (size_t)n);
+  const int s = (int)(q / (size_t)n);
+  const Fp a = reinterpret_cast<const Fp*>(&tab[s])[j];
+  const Fp b = sc[2 * c + (j >> 1)];
+  Fp o;
+  fp_mul(o, a, b);
+  uint2* dst = (uint2*)__builtin_assume_aligned(ev + t, 8);
+#pragma unroll
+  for (int i = 0; i < 5; i++) dst[i] = make_uint2(o.l[2 * i], o.l[2 * i + 1]);
+}
+
+// The evaluated line reaches the team's registers FB, FC through one VGPR
+// element per lane (lane tl < 4 holds Fp tl), read from HBM one publication
+// ahead so the read's latency overlaps the rounds between.
+struct EvPipe {
+  Fp c;
+};
+HG_DEV void ev_fetch(const Team& T, EvPipe& P, const Fp* ev, int n, int ci, int s) {
+  if (T.tl < 4) {
+    const uint2* src = (const uint2*)__builtin_assume_aligned(ev + ((size_t)s * n + ci) * 4 + T.tl, 8);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const uint2 x = src[i];
+      P.c.l[2 * i] = x.x;
+      P.c.l[2 * i + 1] = x.y;
+    }
+  }
+}
+// the held line into FB, FC, then line `next` into flight
+HG_DEV void ev_publish(const Team& T, uint32_t* F, EvPipe& P, const Fp* ev, int n, int ci, int next) {
+  if (T.tl < 4) st_fp_a8(F + (R_FB_x + T.tl) * 10, P.c.l);
+  team_sync();
+  if (next < kNumLines) ev_fetch(T, P, ev, n, ci, next);
+}
+
+using ISqr12T = XInst<XP_SQR12_12_T, S_F, S_F>;
+using ILineT = XInst<XP_LINE_FIX_12_T, S_F, S_F>;
+
+// Miller(G2Base at -sig) over the NAF of 6u + 2 (bn256_gt.hip
+// team_miller_sig's loop; the lines arrive evaluated): f^2, then f * line
+// per digit (two lines on a nonzero digit), then the two Frobenius lines
+HG_DEV void team_miller_sig12(const Team& T, uint32_t* F, const Fp* ev, int n, int ci, XStream& S, XHint after) {
+  const int8_t naf[kNafLen] = HG_NAF;
+  t12_set_one(T, S_F);
+  if (T.tl == 0) {
+    Fp zero, one;
+    fp_zero(zero);
+    fp_one(one);
+    st_fp(F + R_ZERO * 10, zero);
+    st_fp(F + R_ONE * 10, one);
+  }
+  team_sync();
+  EvPipe P;
+  fp_zero(P.c);
+  ev_fetch(T, P, ev, n, ci, 0);
+  int s = 0;
+  for (int i = kNafLen - 1; i > 0; i--) {
+    const int d = naf[i - 1];
+    ev_publish(T, F, P, ev, n, ci, s + 1);  // line s, read by the product after f^2
+    ISqr12T::run(T, S, xh<ILineT>());      // f^2 (f = 1 on the first digit)
+    const XHint after_digit = i > 1 ? xh<ISqr12T>() : xh<ILineT>();
+    if (d != 0) {
+      ILineT::run(T, S, xh<ILineT>());
+      ev_publish(T, F, P, ev, n, ci, s + 2);  // line s + 1 (the addition's)
+      ILineT::run(T, S, after_digit);
+      s += 2;
+    } else {
+      ILineT::run(T, S, after_digit);
+      s += 1;
+    }
+  }
+  // the two Frobenius lines
+  ev_publish(T, F, P, ev, n, ci, s + 1);
+  ILineT::run(T, S, xh<ILineT>());
+  ev_publish(T, F, P, ev, n, ci, kNumLines);
+  ILineT::run(T, S, after);
+}
+
+// fe[r] = FE(Miller(G2Base at -sig_r)) on layout T (kSigTTeamElems elements
+// per team: 18.8 KB of LDS per wave), five teams per wave. The final
+// exponentiation parks two values per check in HBM: fe[r] itself (the result
+// overwrites it) and park[r]. kPad: one pairing wave per SIMD (as
+// k_verify_sig's default); unpadded, two batches' waves share a SIMD.
+template <bool kPad>
+__global__ __launch_bounds__(64, kPad ? 1 : 2) void k_verify_sig12(const Fp* ev, int n, Gt* fe, Gt* park) {
+  constexpr int kWords = kSigTTeamElems * 10;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams12 * kWords];
+  // beside the GT fold on another stream: the pairing wave (the step's
+  // critical path) wins the issue arbitration
+  __builtin_amdgcn_s_setprio(3);
+  if constexpr (kPad) asm volatile("" ::: "v255", "a0");
+  Team T = make_team12(lds, kWords);
+  uint32_t* F = T.base + kSigTRegBase * 10;
+  const int idx = blockIdx.x * kTeams12 + team12_index();
+  const bool valid = idx < n;
+  const int ci = valid ? idx : n - 1;
+  XStream S = x_stream();
+  team_miller_sig12(T, F, ev, n, ci, S, SigFE<SigProgs12>::final_exp_hint_t());
+  // parking records: res in fe[idx] (the result overwrites it), t0 in
+  // park[idx]; a padding team (idx >= n) uses spare records park[n + ...]
+  // (park has n + kTeams12 + 1 records). Recomputed at each use.
+  SigFE<SigProgs12>::team_final_exp_fc_t(T, S, [=](int k) -> uint32_t* {
+    const int i = blockIdx.x * kTeams12 + team12_index();
+    if (k == 0) return (i < n ? fe + i : park + n + 1 + (i - n))->w;
+    return (i < n ? park + i : park + n + 1 + kTeams12 + (i - n))->w;
+  });
+  team_sync();
+  Fp v;
+  ld_fp_a8(v, slot(T, S_F) + T.e * 10);
+  if (valid && T.active) {
+    uint2* dst = (uint2*)__builtin_assume_aligned(fe[idx].w + 10 * T.e, 8);
+#pragma unroll
+    for (int i = 0; i < 5; i++) dst[i] = make_uint2(v.l[2 * i], v.l[2 * i + 1]);
+  }
+}
+
+bool sig12_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("HG_SIG12");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// the evaluated lines, then (each 256-byte aligned) the parking records and
+// the signatures' scalars
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+static size_t sig12_park_offset(int n) { return align256((size_t)n * kNumLines * 4 * sizeof(Fp)); }
+static size_t sig12_scalar_offset(int n) {
+  return sig12_park_offset(n) + align256((size_t)(n + 1 + 2 * kTeams12) * sizeof(Gt));
+}
+size_t sig12_lines_bytes(int n) { return sig12_scalar_offset(n) + (size_t)n * 2 * sizeof(Fp); }
+
+void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Fp* ev, Gt* fe,
+                          hipStream_t s, bool pad) {
+  if (n <= 0) return;
+  Gt* park = (Gt*)((uint8_t*)ev + sig12_park_offset(n));
+  Fp* sc = (Fp*)((uint8_t*)ev + sig12_scalar_offset(n));
+  k_sig_scalars<<<(n + 255) / 256, 256, 0, s>>>(sigs, flavor, n, sc);
+  const size_t items = (size_t)n * kNumLines * 4;
+  k_sig_lines<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(sc, n, tab, ev);
+  const int blocks = (n + kTeams12 - 1) / kTeams12;
+  if (pad) k_verify_sig12<true><<<blocks, 64, 0, s>>>(ev, n, fe, park);
+  else k_verify_sig12<false><<<blocks, 64, 0, s>>>(ev, n, fe, park);
+}
+
+}  // namespace hg

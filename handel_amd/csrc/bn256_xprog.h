@@ -458,21 +458,4 @@ using IMul12S = XInst<XP_MUL12_S, D, A, B>;
 template <int D, int A>
 using ICycS = XInst<XP_CYC_SQR_X_S, D, A>;
 
-// t12_pow_v_x on layout S: dst = a^v with the conjugate of a in slot SK
-template <int D, int SA, int SK>
-HG_DEV void t12_pow_v_s(const Team& T, XStream& S, XHint h) {
-  static_assert(D != SA && D != SK && SA != SK, "scratch slot");
-  t12_conj(T, SK, SA);                            // a^-1
-  ICycS<D, SA>::run(T, S, xh<ICycS<D, D>>());    // a^2
-  const int nsq[4] = {2, 3, 7, 8};
-#pragma unroll 1
-  for (int seg = 0; seg < 4; seg++) {
-    const XHint mul = seg == 0 ? xh<IMul12S<D, D, SK>>() : xh<IMul12S<D, D, SA>>();
-#pragma unroll 1
-    for (int i = 0; i < nsq[seg]; i++) ICycS<D, D>::run(T, S, i + 1 < nsq[seg] ? xh<ICycS<D, D>>() : mul);
-    if (seg == 0) IMul12S<D, D, SK>::run(T, S, xh<ICycS<D, D>>());
-    else IMul12S<D, D, SA>::run(T, S, seg < 3 ? xh<ICycS<D, D>>() : h);
-  }
-}
-
 }  // namespace hg

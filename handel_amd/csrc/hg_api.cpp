@@ -166,6 +166,7 @@ struct Ws {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   DevBuf<Gt> gt_fe;
+  DevBuf<uint8_t> sig_lines;  // launch_sig_pairing12: the batch's lines evaluated at -sig
   void release() {
     pts2.release();
     pts1.release();
@@ -182,6 +183,7 @@ struct Ws {
     gt_partial.release();
     gt_y.release();
     gt_fe.release();
+    sig_lines.release();
     if (side) (void)hipStreamDestroy(side);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
@@ -192,7 +194,8 @@ struct Ws {
     return pts2.cap * sizeof(PointG2) + pts1.cap * sizeof(PointG1) + checks.cap * sizeof(CheckIn) +
            (codes_b.cap + codes_c.cap) * sizeof(int32_t) + order.cap * sizeof(int) + agg_ws.cap +
            gt_plan.cap * sizeof(GtReq) + gt_hdr.cap * sizeof(GtHdr) + gt_terms.cap * sizeof(uint32_t) +
-           gt_ord.cap * sizeof(int2) + gt_multi.cap * sizeof(int) + (gt_partial.cap + gt_y.cap + gt_fe.cap) * sizeof(Gt);
+           gt_ord.cap * sizeof(int2) + gt_multi.cap * sizeof(int) + (gt_partial.cap + gt_y.cap + gt_fe.cap) * sizeof(Gt) +
+           sig_lines.cap;
   }
 };
 
@@ -904,13 +907,18 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     if (overlap) {
       HG_CHECK(c, ensure_side(ws));
       HG_CHECK(c, ws.gt_fe.ensure(n));
+      if (sig12_enabled()) HG_CHECK(c, ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
     }
     if (overlap) {
       // s:    pairing (decodes its signatures) ............ -> wait -> compare
       // side: wait -> prologue (codes, counters), plan, chunks, combine -> join
       HG_CHECK(c, hipEventRecord(ws.ev_fork, s));
       PhaseTimer t(c, HG_PHASE_VERIFY, s);
-      launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s, lane ? lane->pad : true);
+      if (sig12_enabled())
+        launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)ws.sig_lines.p, ws.gt_fe.p, s,
+                             lane ? lane->pad : true);
+      else
+        launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s, lane ? lane->pad : true);
       t.stop();
       HG_CHECK(c, hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
       launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, ws.pts1.p, d_codes, (int*)gw.hdr,
@@ -1760,6 +1768,7 @@ int hg_lane_create(hg_ctx* c, size_t max_batch, size_t max_words, int overlap, h
   if (e == hipSuccess) e = w.gt_partial.ensure(chunks);
   if (e == hipSuccess) e = w.gt_y.ensure(n);
   if (e == hipSuccess) e = w.gt_fe.ensure(n);
+  if (e == hipSuccess && sig12_enabled()) e = w.sig_lines.ensure(sig12_lines_bytes((int)n));
   if (e == hipSuccess && l->overlap) e = ensure_side(w);
   if (e != hipSuccess) {
     c->err = std::string("hg_lane_create: ") + hipGetErrorString(e);

@@ -1,6 +1,7 @@
-"""k_verify_sig's final exponentiation on layout S (bn256_gt.hip
-team_final_exp_fc_s, bn256_xprog.h t12_pow_v_s): the chain runs over seven
-Fp12 slots, with several slots reused for different values along the way.
+"""The sig-only pairing kernels' final exponentiation on layout S
+(bn256_sigfe.h SigFE::team_final_exp_fc_s and SigFE::t12_pow_v_s, shared by
+k_verify_sig and k_verify_sig12): the chain runs over seven Fp12 slots, with
+several slots reused for different values along the way.
 
 This test reads the two device functions' text, turns their statements into
 operations on a slot dictionary (Fp12 values from the oracle) and runs them:
@@ -62,6 +63,12 @@ def _to_python(body):
             m = re.match(r"t12_(conj|frob|frob2|copy)\(T, S_(\w), S_(\w)\)$", s)
             if m:
                 return f"{m.group(1)}('{m.group(2)}', '{m.group(3)}')"
+            m = re.match(r"t12_park\(T, S_(\w), park\((\d)\)\)$", s)
+            if m:
+                return f"park('{m.group(1)}', {m.group(2)})"
+            m = re.match(r"t12_unpark\(T, S_(\w), park\((\d)\)\)$", s)
+            if m:
+                return f"unpark('{m.group(1)}', {m.group(2)})"
             m = re.match(r"t12_inv_norm\(T, S_(\w)\)$", s)
             if m:
                 return f"inv('{m.group(1)}')"
@@ -120,9 +127,16 @@ def _to_python(body):
     return "\n".join(out)
 
 
-def test_final_exp_layout_s_matches_oracle():
-    fc_src = _to_python(_body(os.path.join(CSRC, "bn256_gt.hip"), "HG_DEV void team_final_exp_fc_s("))
-    pow_src = _to_python(_body(os.path.join(CSRC, "bn256_xprog.h"), "HG_DEV void t12_pow_v_s("))
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("layout,slots_used", [("s", "FABCDEG"), ("t", "FABCD")])
+def test_final_exp_layout_matches_oracle(layout, slots_used):
+    """layout s: k_verify_sig's seven slots; layout t: k_verify_sig12's five
+    slots, two values parked in HBM (t12_park / t12_unpark)."""
+    fc_src = _to_python(_body(os.path.join(CSRC, "bn256_sigfe.h"),
+                              f"HG_DEV static void team_final_exp_fc_{layout}("))
+    pow_src = _to_python(_body(os.path.join(CSRC, "bn256_sigfe.h"), "HG_DEV static void t12_pow_v_s("))
     rng = random.Random(5)
     f = [(rng.randrange(O.P), rng.randrange(O.P)) for _ in range(6)]
     slots = {}
@@ -148,7 +162,16 @@ def test_final_exp_layout_s_matches_oracle():
     def sqr(d, a):
         slots[d] = O.f12_sqr(slots[a])
 
-    env = {"conj": conj, "frob": frob, "frob2": frob2, "copy": copy, "inv": inv, "mul": mul, "sqr": sqr}
+    parked = {}
+
+    def park(a, k):
+        parked[k] = slots[a]
+
+    def unpark(d, k):
+        slots[d] = parked.pop(k)  # read once, after it was written
+
+    env = {"conj": conj, "frob": frob, "frob2": frob2, "copy": copy, "inv": inv, "mul": mul, "sqr": sqr,
+           "park": park, "unpark": unpark}
 
     def powv(d, sa, sk):
         assert len({d, sa, sk}) == 3
@@ -157,8 +180,9 @@ def test_final_exp_layout_s_matches_oracle():
         assert slots[d] == O.f12_pow(slots[sa], V), "t12_pow_v_s"
 
     env["powv"] = powv
-    for s in "FABCDEG":  # garbage everywhere but F
+    for s in slots_used:  # garbage everywhere but F
         slots[s] = O.f12_pow(f, rng.randrange(2, 1000)) if s != "F" else f
     exec(fc_src, dict(env))
-    assert set(slots) == set("FABCDEG"), "layout S uses slots F..G only"
+    assert set(slots) == set(slots_used), f"layout {layout} uses slots {slots_used} only"
+    assert not parked, "every parked value is taken back"
     assert slots["F"] == O.final_exponentiation_fc(f)

@@ -518,6 +518,15 @@ PROGRAMS["SDBL"] = [prog_sqr12()[0] + fixed_line_eval()]
 PROGRAMS["LFEV"] = [prog_line_n("FB", "FC")[0] + fixed_line_eval()]
 # Fp12 product in the compact GT-fold team layout (context FOLD below)
 PROGRAMS["MUL12F"] = prog_mul12()
+# k_verify_sig12 (bn256_sig12.hip): the sig-only pairing on FIVE 12-lane teams
+# per wave (make_team12). The G2Base lines arrive evaluated at -sig
+# (k_sig_lines), so the Miller loop is f^2 (SQR12) and f * line (LINE_FIX)
+# with nothing beside them on lanes 12..15, and every pre-pass value lives on
+# lanes 0..11 (PRE_LANES).
+PROGRAMS["SQR12_12"] = prog_sqr12()
+PROGRAMS["LINE_FIX_12"] = prog_line_n("FB", "FC")
+PROGRAMS["MUL12_12"] = prog_mul12()
+PROGRAMS["CYC_SQR_X_12"] = prog_cyc_sqr_x()
 # programs also emitted in the single-phase table format (bn256_g2sched.h)
 LEGACY = ("DBL", "ADD_POS", "ADD_NEG", "ADD_F1", "ADD_F2", "CYC_SQR", "SQR12")
 
@@ -652,7 +661,7 @@ assert all(a <= b for a, b in zip(LAZY_LIMB, P2N)), "the negation constant must 
 # output must be a team program, which takes elements below 2p: in
 # t12_pow_v_x and team_final_exp (bn256_xprog.h, bn256_pairing.h) each
 # squaring feeds the next squaring or a MUL12, whose result is canonical.
-LAZY_PROGRAMS = ("CYC_SQR_X",)
+LAZY_PROGRAMS = ("CYC_SQR_X", "CYC_SQR_X_12")
 
 
 def _xsrc(r):
@@ -918,7 +927,7 @@ def run_xround(xr, F, A, B):
 X_FETCH_WORDS = 16  # words per lane one table prefetch brings in (>= the widest round)
 # programs whose pre-pass values live on lanes 0..11 only, so that they also
 # run in 12-lane teams (five per wave: k_gt_chunks, make_team12)
-PRE_LANES = {"MUL12F": 12}
+PRE_LANES = {"MUL12F": 12, "SQR12_12": 12, "LINE_FIX_12": 12, "MUL12_12": 12, "CYC_SQR_X_12": 12}
 KARATSUBA_MIN = 4   # jobs of this many products use Karatsuba (when check_xround allows)
 # FE: the register file from register 2 on; ML: slots C..J during the Miller loop
 # FOLD: the GT fold kernels' compact team region (bn256_gt.hip): slots F, A, B,
@@ -932,6 +941,7 @@ X_PROGRAMS = {  # name -> (program, scratch context)
     "MADD_F2_2": "ML", "PADD_F2_3": "ML",
     "SQR12": "ML", "LINE_PK": "ML", "LINE_FIX": "ML", "CYC_SQR": "FE", "MUL12": "FE", "CYC_SQR_X": "FE",
     "FEVAL": "ML", "SDBL": "ML", "LFEV": "ML", "MUL12F": "FOLD",
+    "SQR12_12": "ML", "LINE_FIX_12": "ML", "MUL12_12": "FE", "CYC_SQR_X_12": "FE",
 }
 
 
@@ -1104,6 +1114,13 @@ def validate_x(seed=2):
         assert unflat(run_xprogram(X["CYC_SQR_X"], dict(F), flat(cyc))) == O.f12_sqr(cyc), "xCYC_SQR_X"
         assert unflat(run_xprogram(X["MUL12"], dict(F), flat(f), flat(g))) == O.f12_mul(f, g), "xMUL12"
         assert unflat(run_xprogram(X["MUL12F"], dict(F), flat(f), flat(g))) == O.f12_mul(f, g), "xMUL12F"
+        # the 12-lane (pre-pass on lanes 0..11) forms of k_verify_sig12
+        assert unflat(run_xprogram(X["SQR12_12"], dict(F), flat(f))) == O.f12_sqr(f), "xSQR12_12"
+        assert unflat(run_xprogram(X["CYC_SQR_X_12"], dict(F), flat(cyc))) == O.f12_sqr(cyc), "xCYC_SQR_X_12"
+        assert unflat(run_xprogram(X["MUL12_12"], dict(F), flat(f), flat(g))) == O.f12_mul(f, g), "xMUL12_12"
+        for name in ("SQR12_12", "LINE_FIX_12", "MUL12_12", "CYC_SQR_X_12"):
+            for xr in X[name]:  # no pre-pass value on lanes 12..15
+                assert all(d == NONE for L in xr.lanes[12:] for d, _ in L["pre"]), name
         G = dict(F)
         la, lb, lc = [(rng.randrange(P), rng.randrange(P)) for _ in range(3)]
         put(G, "LA", la)
@@ -1113,6 +1130,8 @@ def validate_x(seed=2):
         put(G, "FB", lb)
         put(G, "FC", lc)
         assert unflat(run_xprogram(X["LINE_FIX"], G, flat(f))) == O._mul_line(f, O.F2_ONE, lb, lc), "xLINE_FIX"
+        assert unflat(run_xprogram(X["LINE_FIX_12"], G, flat(f))) == O._mul_line(f, O.F2_ONE, lb, lc), \
+            "xLINE_FIX_12"
     return X
 
 
@@ -1187,7 +1206,28 @@ SIG_INSTANCES = sorted(set(
     # t3 = t2^2 as a product (canonical, 21 scratch elements: the canonical
     # CYC_SQR's 34 would set the region's end)
     + [("MUL12", ("D", "C", "C"))]))
-ALL_INSTANCES = [(n, b, "") for n, b in INSTANCES] + [(n, b, "S") for n, b in SIG_INSTANCES]
+# k_verify_sig12's team region (layout "T", bn256_sig12.hip): FIVE Fp12 slots
+# F, A, B, C, D — the final exponentiation parks two values (res and t0) in
+# HBM while the exponentiations by u run (bn256_sigfe.h team_final_exp_fc_t),
+# so five slots are live at most — then the register file (ZERO, ONE; the
+# Miller loop's FB, FC; the final exponentiation's pre-pass scratch from
+# register 2 on). 94 elements: five 12-lane teams take 18.8 KB of LDS per
+# wave, so a CU holds eight pairing waves (two per SIMD) and a fold workgroup.
+SIG_T_SLOTS = SLOTS[:5]
+SIG_T_F_BASE = 12 * len(SIG_T_SLOTS)
+SIG_T_SCR_BASE = {"FE": SIG_T_F_BASE + 2, "ML": 12 * SLOTS.index("A")}
+SIG_T_INSTANCES = sorted(set(
+    [("SQR12_12", ("F", "F")), ("LINE_FIX_12", ("F", "F"))]
+    # the easy part and the three phases' exponentiations by v (C <-> D, the
+    # conjugate of the base in B / F) and their tails
+    + [("MUL12_12", b) for b in [("B", "F", "D"), ("A", "D", "B"), ("F", "B", "A"), ("F", "F", "A"),
+                                 ("C", "C", "B"), ("C", "C", "F"), ("D", "D", "B"), ("D", "D", "F"),
+                                 ("B", "A", "B"), ("B", "A", "F"), ("D", "A", "A"), ("D", "B", "C"),
+                                 ("F", "A", "D"), ("F", "A", "F"), ("F", "C", "F"), ("D", "D", "C"), ("C", "C", "D")]]
+    + [("CYC_SQR_X_12", b) for b in [("C", "F"), ("C", "C"), ("D", "C"), ("D", "D"), ("C", "D"), ("C", "B"),
+                                     ("A", "A"), ("B", "A")]]))
+ALL_INSTANCES = ([(n, b, "") for n, b in INSTANCES] + [(n, b, "S") for n, b in SIG_INSTANCES]
+                 + [(n, b, "T") for n, b in SIG_T_INSTANCES])
 
 
 
@@ -1204,6 +1244,9 @@ def bind(xr, binding, ctx, layout=""):
     if layout == "S":
         assert ctx in SIG_SCR_BASE and all(b in SIG_SLOTS for b in binding), "layout S: slots F..G only"
         sbase, fbase, region_end = SIG_SCR_BASE[ctx], SIG_F_BASE, SIG_F_BASE + NREGS_RUNTIME
+    if layout == "T":
+        assert ctx in SIG_T_SCR_BASE and all(b in SIG_T_SLOTS for b in binding), "layout T: slots F..D only"
+        sbase, fbase, region_end = SIG_T_SCR_BASE[ctx], SIG_T_F_BASE, SIG_T_F_BASE + NREGS_RUNTIME
 
     def src(code):
         if code >= X_SCR:
@@ -1240,6 +1283,8 @@ def bind(xr, binding, ctx, layout=""):
             assert v == NONE or v < region_end, "index out of the kernels' team region"
         if layout == "S" and ctx == "ML":  # the Miller scratch stays inside slots A..G
             assert all(d == NONE or 12 <= d < SIG_F_BASE for d, _ in L["pre"]), "layout S: ML scratch"
+        if layout == "T" and ctx == "ML":  # ... inside slots A..D
+            assert all(d == NONE or 12 <= d < SIG_T_F_BASE for d, _ in L["pre"]), "layout T: ML scratch"
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
     out.ks1, out.ks2 = xr.ks1, xr.ks2
@@ -1269,7 +1314,7 @@ def check_instances(X, seed=3):
     rng = random.Random(seed)
     for name, binding, layout in ALL_INSTANCES:
         ctx = X_PROGRAMS[name]
-        fb = SIG_F_BASE if layout == "S" else F_BASE_CTX[ctx]
+        fb = SIG_F_BASE if layout == "S" else (SIG_T_F_BASE if layout == "T" else F_BASE_CTX[ctx])
         rounds = [bind(xr, binding, ctx, layout) for xr in X[name]]
         mem = [rng.randrange(P) for _ in range(F_BASE + NREGS)]
         mem[fb + REG["ZERO"]] = 0
@@ -1293,7 +1338,8 @@ def check_instances(X, seed=3):
 # the programs k_verify_sig runs (bn256_gt.hip: the sig-only Miller loop and
 # the final exponentiation); its team region ends after the last element they
 # (and the hand-written helpers: registers up to FC) touch
-SIG_PROGRAMS = ("SDBL", "LFEV", "FEVAL", "LINE_FIX", "MUL12", "CYC_SQR_X", "CYC_SQR")
+SIG_PROGRAMS = ("SDBL", "LFEV", "FEVAL", "LINE_FIX", "MUL12", "CYC_SQR_X", "CYC_SQR",
+                "SQR12_12", "LINE_FIX_12", "MUL12_12", "CYC_SQR_X_12")
 
 
 def touched(bx):
@@ -1310,6 +1356,7 @@ def touched(bx):
 
 def emit_x(X, path):
     sig_end = SIG_F_BASE + REG["FC.y"] + 1  # team_miller_sig's registers: ZERO .. FC
+    sig_t_end = SIG_T_F_BASE + REG["FC.y"] + 1  # team_miller_sig12's: ZERO, ONE, FB, FC
     fold_end = FOLD_F_BASE + 2               # ZERO, ONE
     for name, binding, layout in ALL_INSTANCES:
         ctx = X_PROGRAMS[name]
@@ -1317,21 +1364,27 @@ def emit_x(X, path):
             t = touched(bind(xr, binding, ctx, layout)) + 1
             if layout == "S":
                 sig_end = max(sig_end, t)
+            if layout == "T":
+                sig_t_end = max(sig_t_end, t)
             if ctx == "FOLD":
                 fold_end = max(fold_end, t)
     sig_names = sorted({n for n, _, lay in ALL_INSTANCES if lay == "S"}, key=list(X_PROGRAMS).index)
+    sig_t_names = sorted({n for n, _, lay in ALL_INSTANCES if lay == "T"}, key=list(X_PROGRAMS).index)
     lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
              "// Two-phase team programs executed by bn256_xprog.h (encoding: see there),",
              "// one table per call-site instance (absolute team element indices).",
              "#pragma once", "#include <stdint.h>", "namespace hg {",
              f"// HG_P2N: ({NEG_MULT}p)'' (the negation constant of pre-pass and linear terms)",
              "#define HG_P2N " + ", ".join("0x%08xu" % v for v in P2N),
-             "enum XProg { " + ", ".join([f"XP_{n}" for n in X_PROGRAMS] + [f"XP_{n}_S" for n in sig_names]) + " };",
+             "enum XProg { " + ", ".join([f"XP_{n}" for n in X_PROGRAMS] + [f"XP_{n}_S" for n in sig_names]
+                                         + [f"XP_{n}_T" for n in sig_t_names]) + " };",
              f"static constexpr int kXFetchWords = {X_FETCH_WORDS};",
              f"static constexpr int kFoldRegBase = {FOLD_F_BASE};  // FOLD team region: ZERO, ONE here",
              f"static constexpr int kFoldTeamElems = {fold_end + fold_end % 2};  // elements the fold programs touch",
              f"static constexpr int kSigRegBase = {SIG_F_BASE};  // k_verify_sig's layout S: registers here",
              f"static constexpr int kSigTeamElems = {sig_end + sig_end % 2};  // k_verify_sig's team region (layout S)",
+             f"static constexpr int kSigTRegBase = {SIG_T_F_BASE};  // k_verify_sig12's layout T: registers here",
+             f"static constexpr int kSigTTeamElems = {sig_t_end + sig_t_end % 2};  // k_verify_sig12's team region",
              "template <int PROG, int D = -1, int A = -1, int B = -1> struct XInst;"]
     words = []
     for name, binding, layout in ALL_INSTANCES:
@@ -1360,7 +1413,7 @@ def emit_x(X, path):
             calls.append(f"x_round<{bx.nv}, {bx.nt}, {bx.np}, {bx.nl}, {bx.words()}, {bx.np2}, {bx.nl2}, "
                          f"{bx.kp}, {bx.kl1}, {bx.kl2}, {bx.ks1}, {bx.ks2}, {lz}, {bx.ef}, {fu}>(T, S, {off}, {nxt});")
         args = ", ".join(f"S_{b}" for b in binding)
-        targs = f"XP_{name}{'_S' if layout == 'S' else ''}" + (", " + args if args else "")
+        targs = f"XP_{name}{'_' + layout if layout else ''}" + (", " + args if args else "")
         lines.append(f"template <> struct XInst<{targs}> {{ static constexpr int kOff = {rounds[0][1]}, "
                      f"kW = {rounds[0][0].words()}; HG_DEV static void run(const Team& T, XStream& S, XHint h) {{ "
                      + " ".join(calls) + " } };")
