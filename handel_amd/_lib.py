@@ -91,6 +91,7 @@ SIGNATURES = {
     "hg_sign_msg": (_I, [_P, _P, _SZ, _P, _SZ, _P]),
     "hg_debug_fp_mul": (_I, [_P, _P, _P, _SZ, _P]),
     "hg_diag_read": (_I, [_P, _P, _SZ]),
+    "hg_sig_pairing_device": (_I, [_P, _P, _SZ, _P, _I, _P]),
     "hg_debug_fp12": (_I, [_P, _I, _P, _P, _SZ, _P]),
     "hg_timing_enable": (_I, [_P, _I]),
     "hg_timing_read": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),

@@ -79,8 +79,13 @@ void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* 
 size_t sig12_lines_bytes(int n);
 void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Fp* ev, Gt* fe,
                           hipStream_t s, bool pad);
-// the 12-lane kernel is the default; HG_SIG12=0 selects launch_sig_pairing
-bool sig12_enabled();
+// which kernel a submission runs: the 12-lane one for unpadded launches (the
+// throughput mode: batches in flight share the SIMDs, and a check costs 20 %
+// fewer wave-instructions), the 16-lane padded k_verify_sig for padded ones
+// (the latency mode: one wave per SIMD, where its shorter per-wave program
+// and the absence of the line kernels give the lower batch latency).
+// HG_SIG12=1 / 0 forces one kernel for every launch (A/B).
+bool sig12_for(bool pad);
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s);
 // the same, and the verdict bitset (ceil(n / 8) bytes, hg_pack_verdicts_device's layout)
 void launch_gt_compare_bits(const Gt* fe, const Gt* y, int n, int32_t* codes, uint8_t* bits, hipStream_t s);

@@ -183,12 +183,12 @@ __global__ __launch_bounds__(64, kPad ? 1 : 2) void k_verify_sig12(const Fp* ev,
   }
 }
 
-bool sig12_enabled() {
-  static const bool on = [] {
+bool sig12_for(bool pad) {
+  static const int mode = [] {
     const char* e = getenv("HG_SIG12");
-    return !(e && atoi(e) == 0);
+    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return on;
+  return mode == 1 || (mode == -1 && !pad);
 }
 
 // the evaluated lines, then (each 256-byte aligned) the parking records and

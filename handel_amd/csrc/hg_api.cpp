@@ -907,14 +907,14 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     if (overlap) {
       HG_CHECK(c, ensure_side(ws));
       HG_CHECK(c, ws.gt_fe.ensure(n));
-      if (sig12_enabled()) HG_CHECK(c, ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
+      if (sig12_for(lane ? lane->pad : true)) HG_CHECK(c, ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
     }
     if (overlap) {
       // s:    pairing (decodes its signatures) ............ -> wait -> compare
       // side: wait -> prologue (codes, counters), plan, chunks, combine -> join
       HG_CHECK(c, hipEventRecord(ws.ev_fork, s));
       PhaseTimer t(c, HG_PHASE_VERIFY, s);
-      if (sig12_enabled())
+      if (sig12_for(lane ? lane->pad : true))
         launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)ws.sig_lines.p, ws.gt_fe.p, s,
                              lane ? lane->pad : true);
       else
@@ -1549,6 +1549,27 @@ int hg_debug_fp12(hg_ctx* c, int op, const uint8_t* a, const uint8_t* b, size_t 
   return HG_OK;
 }
 
+int hg_sig_pairing_device(hg_ctx* c, const uint8_t* d_sigs, size_t n, uint8_t* d_fe, int kernel, void* stream) {
+  if (!c || (n && (!d_sigs || !d_fe)) || n > (size_t)INT32_MAX || kernel < 0 || kernel > 3) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HG_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  Submission sub(c, s);
+  HG_CHECK(c, sub.start());
+  const bool pad = (kernel & 1) == 0;
+  if (kernel >= 2) {
+    HG_CHECK(c, c->ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
+    launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)c->ws.sig_lines.p, (Gt*)d_fe, s, pad);
+  } else {
+    launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, (Gt*)d_fe, s, pad);
+  }
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HG_CHECK(c, sub.finish());
+  return HG_OK;
+}
+
 int hg_diag_read(hg_ctx* c, uint64_t* out, size_t n) {
   if (!c || !out) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1768,7 +1789,7 @@ int hg_lane_create(hg_ctx* c, size_t max_batch, size_t max_words, int overlap, h
   if (e == hipSuccess) e = w.gt_partial.ensure(chunks);
   if (e == hipSuccess) e = w.gt_y.ensure(n);
   if (e == hipSuccess) e = w.gt_fe.ensure(n);
-  if (e == hipSuccess && sig12_enabled()) e = w.sig_lines.ensure(sig12_lines_bytes((int)n));
+  if (e == hipSuccess && sig12_for(true)) e = w.sig_lines.ensure(sig12_lines_bytes((int)n));
   if (e == hipSuccess && l->overlap) e = ensure_side(w);
   if (e != hipSuccess) {
     c->err = std::string("hg_lane_create: ") + hipGetErrorString(e);
@@ -1859,7 +1880,16 @@ void* hg_lane_stream(hg_lane* l) { return l ? (void*)l->s : nullptr; }
 
 int hg_lane_set_pairing_padding(hg_lane* l, int pad) {
   if (!l) return HG_ERR_ARG;
-  std::lock_guard<std::mutex> g(l->c->mu);
+  hg_ctx* c = l->c;
+  std::lock_guard<std::mutex> g(c->mu);
+  // the unpadded lane runs the 12-lane kernel: its evaluated-line workspace
+  // at the lane's largest batch now (never grown between batches)
+  if (sig12_for(pad != 0)) {
+    HG_CHECK(c, hipSetDevice(c->device));
+    HG_CHECK(c, hipStreamSynchronize(l->s));
+    if (l->ws.side) HG_CHECK(c, hipStreamSynchronize(l->ws.side));
+    HG_CHECK(c, l->ws.sig_lines.ensure(sig12_lines_bytes((int)l->max_batch)));
+  }
   l->pad = pad != 0;
   return HG_OK;
 }

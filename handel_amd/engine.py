@@ -167,6 +167,16 @@ class Engine:
         self._check(self.L.hg_pack_verdicts_device(self.ctx, d_codes, n, d_bits, stream or None),
                     "hg_pack_verdicts_device")
 
+    # hg_sig_pairing_device kernels
+    SIG_K16_PAD, SIG_K16, SIG_K12_PAD, SIG_K12 = 0, 1, 2, 3
+
+    def sig_pairing_device(self, d_sigs: int, n: int, d_fe: int, kernel: int, stream: int = 0):
+        """FE(Miller(G2Base at -sig)) of n signature marshals into d_fe (n x 480
+        bytes) with one chosen pairing kernel (hg_sig_pairing_device): the
+        per-kernel roofline and the cross-kernel check."""
+        self._check(self.L.hg_sig_pairing_device(self.ctx, d_sigs, n, d_fe, int(kernel), stream or None),
+                    "hg_sig_pairing_device")
+
     def verify_aggregate(self, reqs: np.ndarray, words: np.ndarray, sigs: bytes, want_agg: bool = False):
         reqs = np.ascontiguousarray(reqs, dtype=REQ_DTYPE)
         words = np.ascontiguousarray(words, dtype=np.uint64)

@@ -260,6 +260,17 @@ int hg_timing_read_phase(hg_ctx* ctx, int phase, double* total_ms, int* launches
  * 6 conj(a), 7 a^u, 8 final exponentiation, 9/10 table-program squarings. */
 int hg_debug_fp12(hg_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out);
 
+/* Kernel probe of the GT path's signature side (bench.py per-kernel
+ * roofline, the GPU suite's cross-kernel check): d_fe[r] (480 bytes, the
+ * engine's internal GT layout) = FE(Miller(G2Base at -sig_r)) for the n
+ * 64-byte signature marshals at d_sigs (context flavor), computed by kernel
+ * 0: k_verify_sig padded (one wave per SIMD), 1: k_verify_sig unpadded,
+ * 2: k_sig_scalars + k_sig_lines + k_verify_sig12 padded, 3: the same
+ * unpadded (what a lane in flight runs). Enqueued on `stream` (NULL: the
+ * context's), ordered like every submission of the context. Replaces no
+ * reference interface: the product paths choose the kernel themselves. */
+int hg_sig_pairing_device(hg_ctx* ctx, const uint8_t* d_sigs, size_t n, uint8_t* d_fe, int kernel, void* stream);
+
 /* Diagnostic builds only (-DHG_DIAG, tools/diag.py): per-block s_memtime
  * phase counters of the last pairing-check launch; HG_ERR_ARG otherwise. */
 int hg_diag_read(hg_ctx* ctx, uint64_t* out, size_t n);
