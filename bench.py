@@ -982,10 +982,15 @@ def main():
     # time, prologue to comparison (HIP events on the launch stream)
     agg_ms = dt / args.steps * 1e3 if inflight > 1 else ph["submit"]
     impl_fpmul = head.terms * FPMUL_PER_GT_MUL + n * FPMUL_PER_SIG_PAIRING
-    sig_kernel = r"k_verify_sig<4, true, false>" if inflight > 1 else r"k_verify_sig<4, true(, true)?>"
+    # batches in flight run on unpadded lanes: the 12-lane pairing kernel with
+    # its line kernels (bn256_sig12.hip); one batch at a time, the padded
+    # 16-lane k_verify_sig (hg_api.cpp: sig12_for)
+    sig_kernel = (r"k_verify_sig12<false>|k_sig_(lines|scalars)" if inflight > 1
+                  else r"k_verify_sig<4, true(, true)?>")
     roof = roofline(impl_fpmul, agg_ms,
-                    (f"the GT submission, {inflight} batches in flight (timed region per step): " if inflight > 1
-                     else "the GT submission: ") + "k_agg_prologue, k_verify_sig beside the GT fold (k_gt_plan, "
+                    (f"the GT submission, {inflight} batches in flight (timed region per step): k_agg_prologue, "
+                     "k_sig_scalars + k_sig_lines + k_verify_sig12 (12-lane teams)" if inflight > 1
+                     else "the GT submission: k_agg_prologue, k_verify_sig") + " beside the GT fold (k_gt_plan, "
                     "k_gt_chunks, k_gt_combine), k_gt_compare_bits",
                     r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare_bits)|" + sig_kernel,
                     f"implemented work: {head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 "
@@ -994,8 +999,9 @@ def main():
                     rocprof_pattern=sig_kernel + r"|k_gt_compare_bits")
     if inflight > 1:
         roof["frac_rocprof_note"] = (
-            "the same work over the rocprof average LAUNCH duration of the headline's pairing kernel (the unpadded "
-            "variant only the headline's lanes launch) plus the comparison, in the driver-invocation profile: with "
+            "the same work over the rocprof average LAUNCH duration of the headline's pairing kernels (k_verify_sig12<false> "
+            "and its line kernels, which only the headline's unpadded lanes launch) plus the comparison, in the "
+            "driver-invocation profile: with "
             f"{inflight} batches in flight two launches share the SIMDs, so a launch lasts longer than a step and "
             "this per-launch fraction is below `frac`")
         roof["sequential_submit_ms"] = round(ph["submit"], 4)
@@ -1018,6 +1024,28 @@ def main():
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
                            "+ final exponentiation, oracle op count); kernel alone (fold not beside it)",
                            rocprof_pattern=r"k_verify_sig<4, true(, (true|false))?>")
+    # the headline's pairing kernel alone: k_sig_scalars + k_sig_lines +
+    # k_verify_sig12<false> (hg_sig_pairing_device kernel 3) on one stream,
+    # HIP events around 5 launches; one batch occupies 820 of the 1024 SIMDs
+    # with one wave each, so this is its latency-bound rate (in flight, two
+    # batches' waves share a SIMD: the primary roofline's time base)
+    sig_stream = torch.cuda.Stream(dev)
+    d_fe = torch.empty(n * 480, dtype=torch.uint8, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    with torch.cuda.stream(sig_stream):
+        eng.sig_pairing_device(head.d_sigs.data_ptr(), n, d_fe.data_ptr(), Engine.SIG_K12, sig_stream.cuda_stream)
+        ev[0].record(sig_stream)
+        for _ in range(5):
+            eng.sig_pairing_device(head.d_sigs.data_ptr(), n, d_fe.data_ptr(), Engine.SIG_K12, sig_stream.cuda_stream)
+        ev[1].record(sig_stream)
+    torch.cuda.synchronize(dev)
+    sig12_ms = ev[0].elapsed_time(ev[1]) / 5
+    del d_fe
+    roof_sig12 = roofline(n * FPMUL_PER_SIG_PAIRING, sig12_ms, "k_sig_scalars + k_sig_lines + k_verify_sig12<false>",
+                          r"k_verify_sig12<false>|k_sig_(lines|scalars)",
+                          f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (the line "
+                          "evaluations included); one launch alone, one wave per SIMD",
+                          rocprof_pattern=r"k_verify_sig12<false>|k_sig_(lines|scalars)")
     roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph_seq["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
                          r"k_gt_(plan<16>|chunks|combine)",
                          f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each); "
@@ -1196,6 +1224,7 @@ def main():
             "roofline": roof,
             "effective_rate": effective,
             "roofline_k_verify": roof_verify,
+            "roofline_k_verify_sig12": roof_sig12,
             "roofline_gt_fold": roof_fold,
             "setup": {"ms": round(head.setup_ms, 2), "what": "per (message, registry), outside the timed "
                       f"region: e(H, pk_i) for {n_reg} keys + GT products of every 16-key window subset and aligned "

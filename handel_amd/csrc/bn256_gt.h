@@ -43,15 +43,11 @@ struct GtWork {
   int cap;         // entries of ord and partial
   Gt* partial;
   int* multi;      // 2n: the big requests from 0, the mid ones from n (k_gt_combine's order)
-  int chunk_grid;  // workgroups of k_gt_chunks (one wave: kGtChunkTeams teams, or 10 with k6)
-  int k6;          // the 6-lane Karatsuba kernels (k_gt_chunks6 / k_gt_combine6)
+  int chunk_grid;  // workgroups of k_gt_chunks (one wave: kGtChunkTeams teams)
   int chunk;       // terms per chunk
   int win_bits;    // 8 or 16: which window table `win` is
 };
 
-// the 6-lane Karatsuba fold and 16-key table kernels (bn256_k6.h) with
-// HG_GT_K6=1; the 12-lane team programs otherwise (the default: faster)
-bool gt_k6();
 // G_i = e(H, pk_i) for the n registry keys
 void launch_gt_keys(const PointG2* reg, int n, const LineCoef* tab, const PointG1* h, Gt* out, hipStream_t s);
 // w8[256 w + s] = product of G_{8w + j} over the bits j of s (absent keys = 1)

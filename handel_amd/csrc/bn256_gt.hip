@@ -32,7 +32,6 @@
 #include "bn256_agg.h"
 #include "bn256_decode.h"
 #include "bn256_gt.h"
-#include "bn256_k6.h"
 #include "bn256_pairing.h"
 #include "bn256_sigfe.h"
 
@@ -245,40 +244,6 @@ __global__ __launch_bounds__(64) void k_gt_win16(const Gt* w8, int nwin8, int nw
   }
 }
 
-// The same on 6-lane Karatsuba teams (bn256_k6.h): ten (window, hi) tasks per
-// wave; the hi value is the right factor of all 256 products, put once.
-__global__ __launch_bounds__(64, 2) void k_gt_win16_6(const Gt* w8, int nwin8, int nwin16, Gt* w16) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams6 * kT6Words];
-  const Team6 T = make_team6(lds);
-  const int task = blockIdx.x * kTeams6 + team6_index();
-  const bool valid = task < 256 * nwin16;
-  const int w = valid ? task >> 8 : 0, hi = task & 255;
-  const Gt* lo_tab = w8 + (size_t)(2 * w) * 256;
-  const bool has_hi = 2 * w + 1 < nwin8;
-  Gt* dst = w16 + (size_t)w * 65536 + (size_t)hi * 256;
-  Fp hx, hy, nx, ny;
-  k6_read(hx, hy, w8 + (size_t)(has_hi ? 2 * w + 1 : 2 * w) * 256 + hi, T);
-  k6_keep_or_one(hx, hy, has_hi, T);
-  k6_put_b(T, hx, hy, false);
-  k6_read(nx, ny, lo_tab, T);
-#pragma unroll 1
-  for (int lo = 0; lo < 256; lo++) {
-    k6_put_a(T, nx, ny, false);
-    if (lo + 1 < 256) k6_read(nx, ny, lo_tab + lo + 1, T);
-    k6_mul(T);
-    if (valid) k6_store(T, dst + lo);
-  }
-}
-
-// The 6-lane fold is opt-in (HG_GT_K6=1): measured slower than the 12-lane
-// kernels (profiles/r04_k6_ab.json)
-bool gt_k6() {
-  static const bool on = [] {
-    const char* e = getenv("HG_GT_K6");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 
 // Block products, one level: dst[j] = src[2j] * src[2j + 1] (the last block of
 // a level may be clipped: src[2j + 1] absent -> 1). src entries `stride` apart.
@@ -585,116 +550,6 @@ __global__ __launch_bounds__(64) void k_gt_combine(int n, const GtHdr* hdr, cons
   if (team == 0) gt_store(T, S_A, y + r);
 }
 
-// The same two kernels on 6-lane teams with Karatsuba Fp2 products
-// (bn256_k6.h): ten teams per wave, 108 instead of 144 Fp products per Fp12
-// product. Same chunk list, same partials, same Y (every value canonical).
-__global__ __launch_bounds__(64, 2) void k_gt_chunks6(const Gt* win, const Gt* blk, const uint32_t* terms,
-                                                   const int2* ord, int cap, const GtReq* plan, const GtHdr* hdr,
-                                                   int chunk, Gt* partial, Gt* y) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams6 * kT6Words];
-  const Team6 T = make_team6(lds);
-  const int team = team6_index();
-  const int total = hdr->chunks, nlong = hdr->nlong;
-  for (int base = blockIdx.x * kTeams6; base < total; base += gridDim.x * kTeams6) {  // wave-uniform
-    const int k = base + team;
-    const bool valid = k < total && T.active;
-    int first = 0, cnt = 0, r = 0, c = 0;
-    bool single = false;
-    if (valid) {
-      const int2 e = k < nlong ? ord[k] : ord[cap - 1 - (k - nlong)];
-      c = e.x;
-      r = e.y;
-      const GtReq g = plan[r];
-      first = g.term_off + (c - g.chunk_off) * chunk;
-      cnt = min(chunk, g.term_off + g.m - first);
-      single = g.chunks == 1;
-    }
-    int maxc = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) maxc = max(maxc, __shfl_xor(maxc, d));
-    // the chunk's term words, read once: lane tl holds terms tl and tl + 6
-    // (terms past 12 are read from the list)
-    const uint32_t my0 = T.tl < cnt ? terms[first + T.tl] : 0u;
-    const uint32_t my1 = T.tl + 6 < cnt ? terms[first + 6 + T.tl] : 0u;
-    const int tbase = 6 * team;
-    auto term = [&](int i) -> uint32_t {  // wave-uniform i: every lane runs the shuffles
-      const int src = tbase + (i < 12 ? i % 6 : 0);
-      const uint32_t v0 = (uint32_t)__shfl((int)my0, src, 64), v1 = (uint32_t)__shfl((int)my1, src, 64);
-      return i < 6 ? v0 : (i < 12 ? v1 : (i < cnt ? terms[first + i] : 0u));
-    };
-    Fp cx, cy, nx, ny;
-    fp_zero(nx);
-    fp_zero(ny);
-    const uint32_t t0 = term(0);
-    k6_read(cx, cy, term_ptr(valid ? t0 : 0u, win, blk), T);
-    k6_keep_or_one(cx, cy, valid, T);
-    k6_put_a(T, cx, cy, valid && (t0 & kTermConj) != 0);
-    // the next table value in flight across each product (one product is
-    // thousands of cycles per lane: one value covers the HBM latency)
-    uint32_t t1 = term(1);
-    if (1 < cnt) k6_read(nx, ny, term_ptr(t1, win, blk), T);
-#pragma unroll 1
-    for (int i = 1; i < maxc; i++) {
-      k6_keep_or_one(nx, ny, i < cnt, T);
-      k6_put_b(T, nx, ny, i < cnt && (t1 & kTermConj) != 0);
-      t1 = term(i + 1);
-      if (i + 1 < cnt) k6_read(nx, ny, term_ptr(t1, win, blk), T);
-      k6_mul(T);
-    }
-    team_sync();
-    if (valid) k6_store(T, single ? y + r : partial + c);
-    team_sync();
-  }
-}
-
-// one wave per request of two or more chunks: teams 0..7 multiply every 8th
-// partial, a 3-level tree joins them (teams 8, 9 idle)
-__global__ __launch_bounds__(64) void k_gt_combine6(int n, const GtHdr* hdr, const int* multi, const GtReq* plan,
-                                                    const Gt* partial, Gt* y) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams6 * kT6Words];
-  constexpr int NT = 8;
-  const int b = blockIdx.x, nbig = hdr->big;
-  if (b >= nbig + hdr->mid) return;  // one request per wave: uniform
-  const int r = b < nbig ? multi[b] : multi[n + b - nbig];
-  const GtReq g = plan[r];
-  const Team6 T = make_team6(lds);
-  const int team = team6_index();
-  const bool in = team < NT;
-  const int rounds = (g.chunks + NT - 1) / NT;
-  Fp x, y0, nx, ny;
-  const bool has0 = in && team < g.chunks;
-  k6_read(x, y0, partial + g.chunk_off + (has0 ? team : 0), T);
-  k6_keep_or_one(x, y0, has0, T);
-  k6_put_a(T, x, y0, false);
-  // the team's next partial in flight across the product
-  int c = team + NT;
-  fp_zero(nx);
-  fp_zero(ny);
-  if (in && c < g.chunks) k6_read(nx, ny, partial + g.chunk_off + c, T);
-#pragma unroll 1
-  for (int i = 1; i < rounds; i++) {
-    k6_keep_or_one(nx, ny, in && c < g.chunks, T);
-    k6_put_b(T, nx, ny, false);
-    c += NT;
-    if (in && c < g.chunks) k6_read(nx, ny, partial + g.chunk_off + c, T);
-    k6_mul(T);
-  }
-  const int span = g.chunks < NT ? g.chunks : NT;
-  for (int d = 1; d < span; d <<= 1) {
-    team_sync();
-    // team t takes team t ^ d's product into B (teams 8, 9 copy their own)
-    const int src = in ? (team ^ d) : team;
-    const uint32_t* from = lds + src * kT6Words + K6_A * kFp12Words + 20 * T.k;
-    Fp bx, by;
-    ld_fp_a8(bx, from);
-    ld_fp_a8(by, from + 10);
-    k6_put_b(T, bx, by, false);
-    k6_mul(T);
-  }
-  team_sync();
-  if (team == 0) k6_store(T, y + r);
-}
-
 // ------------------------------------------------------------------ the pairing check
 // f = Miller(G2Base at -sig) (x/crypto optate.go miller with the G2Base lines
 // from the table): per doubling f^2 with the line's evaluation at -sig beside
@@ -894,8 +749,7 @@ void launch_gt_windows8(const Gt* key, int nreg, Gt* w8, int nwin8, hipStream_t 
 }
 void launch_gt_windows16(const Gt* w8, int nwin8, Gt* w16, int nwin16, hipStream_t s) {
   if (nwin16 <= 0) return;
-  if (gt_k6()) k_gt_win16_6<<<nblk(256 * nwin16, kTeams6), 64, 0, s>>>(w8, nwin8, nwin16, w16);
-  else k_gt_win16<<<nblk(256 * nwin16, kTeams12), 64, 0, s>>>(w8, nwin8, nwin16, w16);
+  k_gt_win16<<<nblk(256 * nwin16, kTeams12), 64, 0, s>>>(w8, nwin8, nwin16, w16);
 }
 void launch_gt_blocks(const Gt* src, int stride, int nsrc, Gt* dst, int ndst, hipStream_t s) {
   if (ndst > 0) k_gt_blocks<<<nblk(ndst, 4), 64, 0, s>>>(src, stride, nsrc, dst, ndst);
@@ -910,13 +764,8 @@ void launch_gt_fold(const AggRequest* reqs, int n, const uint64_t* words, int32_
   else
     k_gt_plan<8><<<nblk(n, kPlanWaves), 64 * kPlanWaves, 0, s>>>(reqs, n, words, codes, nreg, levels, bi, w.plan,
                                                                  w.hdr, w.terms, w.ord, w.cap, w.chunk, w.multi);
-  if (w.k6) {
-    k_gt_chunks6<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.ord, w.cap, w.plan, w.hdr, w.chunk, w.partial, y);
-    k_gt_combine6<<<n, 64, 0, s>>>(n, w.hdr, w.multi, w.plan, w.partial, y);
-  } else {
-    k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.ord, w.cap, w.plan, w.hdr, w.chunk, w.partial, y);
-    k_gt_combine<<<n, 64, 0, s>>>(n, w.hdr, w.multi, w.plan, w.partial, y);
-  }
+  k_gt_chunks<<<w.chunk_grid, 64, 0, s>>>(win, blk, w.terms, w.ord, w.cap, w.plan, w.hdr, w.chunk, w.partial, y);
+  k_gt_combine<<<n, 64, 0, s>>>(n, w.hdr, w.multi, w.plan, w.partial, y);
 }
 void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt* y, int32_t* codes, hipStream_t s) {
   if (n > 0) k_verify_sig<4, false><<<nblk(n, 4), 64, 0, s>>>(sigs, nullptr, 0, n, tab, y, nullptr, codes);

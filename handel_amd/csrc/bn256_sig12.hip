@@ -60,20 +60,19 @@ __global__ __launch_bounds__(256) void k_sig_scalars(const uint8_t* sig_bytes, i
 }
 
 // ev[(s * n + c) * 4 + j] = component j of line s at -sig_c: one Montgomery
-// product per thread (FB = bx * x_sig, FC = cy * -y_sig), consecutive threads
-// on consecutive 40-byte results
+// product per thread (FB = bx * x_sig, FC = cy * -y_sig); grid (4n / 256,
+// lines), consecutive threads on consecutive 40-byte results
 __global__ __launch_bounds__(256) void k_sig_lines(const Fp* sc, int n, const LineCoef* tab, Fp* ev) {
-  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (size_t)n * kNumLines * 4) return;
-  const int j = (int)(t & 3);
-  const size_t q = t >> 2;
-  const int c = (int)(q % (size_t)n);
-  const int s = (int)(q / (size_t)n);
+  const int t = blockIdx.x * 256 + threadIdx.x;  // 4 c + j
+  if (t >= 4 * n) return;
+  const int s = blockIdx.y;
+  const int j = t & 3;
+  const int c = t >> 2;
   const Fp a = reinterpret_cast<const Fp*>(&tab[s])[j];
   const Fp b = sc[2 * c + (j >> 1)];
   Fp o;
   fp_mul(o, a, b);
-  uint2* dst = (uint2*)__builtin_assume_aligned(ev + t, 8);
+  uint2* dst = (uint2*)__builtin_assume_aligned(ev + (size_t)s * 4 * n + t, 8);
 #pragma unroll
   for (int i = 0; i < 5; i++) dst[i] = make_uint2(o.l[2 * i], o.l[2 * i + 1]);
 }
@@ -206,8 +205,7 @@ void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef
   Gt* park = (Gt*)((uint8_t*)ev + sig12_park_offset(n));
   Fp* sc = (Fp*)((uint8_t*)ev + sig12_scalar_offset(n));
   k_sig_scalars<<<(n + 255) / 256, 256, 0, s>>>(sigs, flavor, n, sc);
-  const size_t items = (size_t)n * kNumLines * 4;
-  k_sig_lines<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(sc, n, tab, ev);
+  k_sig_lines<<<dim3((4 * n + 255) / 256, kNumLines), 256, 0, s>>>(sc, n, tab, ev);
   const int blocks = (n + kTeams12 - 1) / kTeams12;
   if (pad) k_verify_sig12<true><<<blocks, 64, 0, s>>>(ev, n, fe, park);
   else k_verify_sig12<false><<<blocks, 64, 0, s>>>(ev, n, fe, park);

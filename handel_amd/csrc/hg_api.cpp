@@ -800,10 +800,7 @@ static int ensure_gt_fold(hg_ctx* c, Ws& ws, size_t n, const FoldCaps& caps, GtW
   w.cap = (int)caps.chunks;
   w.multi = ws.gt_multi.p;
   w.partial = ws.gt_partial.p;
-  // the 6-lane Karatsuba fold (bn256_k6.h) with HG_GT_K6=1 (opt-in: measured slower)
-  const int k6 = gt_k6() ? 1 : 0;
-  w.k6 = k6;
-  const size_t per_wg = k6 ? 10 : kGtChunkTeams;
+  const size_t per_wg = kGtChunkTeams;
   // no more chunk workgroups than the batch can have chunks (a small batch
   // would otherwise launch thousands of workgroups that exit at once)
   const size_t need = (caps.chunks + per_wg - 1) / per_wg;

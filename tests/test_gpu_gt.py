@@ -169,21 +169,18 @@ def test_gt_and_g2_paths_agree():
     + two-pairing check (0, and HG_AGG_PATH=g2) — each in a child process."""
     outs = {}
     # gt16c16 / gt16c5: chunks of 16 and 5 terms per fold team (HG_GT_CHUNK):
-    # a 12-lane team (k_gt_chunks) reads terms past 12 from the term list;
-    # *k6: the opt-in 6-lane fold and table build (HG_GT_K6=1, bn256_k6.h)
+    # a 12-lane team (k_gt_chunks) reads terms past 12 from the term list
     runs = (("gt16", {"HG_GT_LEVEL": "2"}), ("gt8", {"HG_GT_LEVEL": "1"}),
             ("g2", {"HG_GT_LEVEL": "0"}), ("g2env", {"HG_AGG_PATH": "g2"}),
             ("gt16c16", {"HG_GT_LEVEL": "2", "HG_GT_CHUNK": "16"}),
             ("gt16c5", {"HG_GT_LEVEL": "2", "HG_GT_CHUNK": "5"}),
-            ("gt16k6", {"HG_GT_LEVEL": "2", "HG_GT_K6": "1"}),
-            ("gt16k6c16", {"HG_GT_LEVEL": "2", "HG_GT_K6": "1", "HG_GT_CHUNK": "16"}),
             # the signature pairing on 12-lane teams (bn256_sig12.hip) on the
             # padded context path too, and the 16-lane kernel everywhere
             ("gt16sig12", {"HG_GT_LEVEL": "2", "HG_SIG12": "1"}),
             ("gt16sig16", {"HG_GT_LEVEL": "2", "HG_SIG12": "0"}))
     for name, env in runs:
         outs[name] = _child(env)
-    assert [outs[k]["level"] for k, _ in runs] == [2, 1, 0, 0, 2, 2, 2, 2, 2, 2]
+    assert [outs[k]["level"] for k, _ in runs] == [2, 1, 0, 0, 2, 2, 2, 2]
     assert all(outs[k]["codes"] == outs["gt16"]["codes"] for k, _ in runs)
     import bench
     from handel_amd.engine import Engine
