@@ -1025,27 +1025,30 @@ def main():
                            "+ final exponentiation, oracle op count); kernel alone (fold not beside it)",
                            rocprof_pattern=r"k_verify_sig<4, true(, (true|false))?>")
     # the headline's pairing kernel alone: k_sig_scalars + k_sig_lines +
-    # k_verify_sig12<false> (hg_sig_pairing_device kernel 3) on one stream,
-    # HIP events around 5 launches; one batch occupies 820 of the 1024 SIMDs
-    # with one wave each, so this is its latency-bound rate (in flight, two
-    # batches' waves share a SIMD: the primary roofline's time base)
+    # k_verify_sig12 on one stream, HIP events around 5 launches. Its padded
+    # form (hg_sig_pairing_device kernel 2): one batch alone occupies 820 of
+    # the 1024 SIMDs with one wave each — the unpadded form alone would let
+    # the dispatcher stack two waves on some SIMDs and leave others empty —
+    # so this is the kernel's latency-bound rate (in flight, two batches'
+    # waves share every SIMD: the primary roofline's time base)
     sig_stream = torch.cuda.Stream(dev)
     d_fe = torch.empty(n * 480, dtype=torch.uint8, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     with torch.cuda.stream(sig_stream):
-        eng.sig_pairing_device(head.d_sigs.data_ptr(), n, d_fe.data_ptr(), Engine.SIG_K12, sig_stream.cuda_stream)
+        eng.sig_pairing_device(head.d_sigs.data_ptr(), n, d_fe.data_ptr(), Engine.SIG_K12_PAD, sig_stream.cuda_stream)
         ev[0].record(sig_stream)
         for _ in range(5):
-            eng.sig_pairing_device(head.d_sigs.data_ptr(), n, d_fe.data_ptr(), Engine.SIG_K12, sig_stream.cuda_stream)
+            eng.sig_pairing_device(head.d_sigs.data_ptr(), n, d_fe.data_ptr(), Engine.SIG_K12_PAD,
+                                   sig_stream.cuda_stream)
         ev[1].record(sig_stream)
     torch.cuda.synchronize(dev)
     sig12_ms = ev[0].elapsed_time(ev[1]) / 5
     del d_fe
-    roof_sig12 = roofline(n * FPMUL_PER_SIG_PAIRING, sig12_ms, "k_sig_scalars + k_sig_lines + k_verify_sig12<false>",
-                          r"k_verify_sig12<false>|k_sig_(lines|scalars)",
+    roof_sig12 = roofline(n * FPMUL_PER_SIG_PAIRING, sig12_ms, "k_sig_scalars + k_sig_lines + k_verify_sig12<true>",
+                          r"k_verify_sig12<true>|k_sig_(lines|scalars)",
                           f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (the line "
                           "evaluations included); one launch alone, one wave per SIMD",
-                          rocprof_pattern=r"k_verify_sig12<false>|k_sig_(lines|scalars)")
+                          rocprof_pattern=r"k_verify_sig12<true>|k_sig_(lines|scalars)")
     roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph_seq["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
                          r"k_gt_(plan<16>|chunks|combine)",
                          f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each); "
