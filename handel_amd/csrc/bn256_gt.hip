@@ -579,7 +579,7 @@ HG_DEV void line_fetch(const Team& T, LinePipe& P, const LineCoef* tab, int s) {
 // into flight
 HG_DEV void publish_line(const Team& T, uint32_t* F, LinePipe& P, const LineCoef* tab, int next) {
   if (T.tl < 4) st_fp(F + (R_FBX_x + T.tl) * 10, P.c);
-  team_sync();
+  team_sync(T);
   if (next < kNumLines) line_fetch(T, P, tab, next);
 }
 
@@ -600,7 +600,7 @@ HG_DEV void team_miller_sig(const Team& T, uint32_t* F, const Fp& sx, const Fp& 
     st_fp(F + R_SX * 10, use_s ? sx : zero);
     st_fp(F + R_NSY * 10, use_s ? nsy : zero);
   }
-  team_sync();
+  team_sync(T);
   LinePipe P;
   fp_zero(P.c);
   line_fetch(T, P, tab, 0);
@@ -690,6 +690,33 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
   team_sync();
   const bool ok = t12_equal(T, S_F, S_A);
   if (valid && T.tl == 0 && codes[idx] == HG_OK) codes[idx] = ok ? HG_OK : HG_ERR_SIG_INVALID;
+}
+
+// The latency form of k_verify_sig<4, true>: each 16-lane team spans the two
+// waves of a 128-thread workgroup (make_team_w2), which split every round's
+// products between them (bn256_xprog.h x_job_split), so a check's dependent
+// chain is about half as long for the same values. Twice the waves per check:
+// it pays when the batch is small (n <= kSigW2MaxN: 2n waves still fit one per
+// SIMD) and the step waits on the pairing — a lone batch's latency.
+static constexpr int kSigW2MaxN = 2048;
+__global__ __launch_bounds__(128) void k_verify_sig_w2(const uint8_t* sig_bytes, int flavor, int n,
+                                                       const LineCoef* tab, Gt* fe) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kSigTeamWords + 4 * 16 * kXchgWords];
+  __builtin_amdgcn_s_setprio(3);
+  // one wave per SIMD: a workgroup's two waves on two SIMDs of the CU
+  asm volatile("" ::: "v255", "a0");
+  Team T = make_team_w2(lds, kSigTeamWords, lds + 4 * kSigTeamWords);
+  uint32_t* F = T.base + kSigRegBase * 10;
+  const int idx = blockIdx.x * 4 + ((threadIdx.x & 63) >> 4);
+  const bool valid = idx < n;
+  const int ci = valid ? idx : n - 1;
+  PointG1 sg;
+  (void)decode_g1_one(sig_bytes + (size_t)ci * 64, flavor, sg);
+  XStream S = x_stream();
+  team_miller_sig(T, F, sg.x, sg.y, sg.inf == 0, tab, S, SigFE<SigProgs16>::final_exp_hint_s());
+  SigFE<SigProgs16>::team_final_exp_fc_s(T, S);
+  team_sync(T);
+  if (valid && T.wave == 0) gt_store(T, S_F, fe + idx);
 }
 
 // fe[r] == y[r] (both canonical: word equality) for every request still HG_OK;
@@ -784,10 +811,26 @@ static int sig_env() {
   }();
   return v;
 }
+// the two-wave teams for a padded launch of at most kSigW2MaxN checks;
+// HG_SIG_W2=0 turns them off (A/B)
+bool sig_w2_for(bool pad, int n) {
+  static const bool on = [] {
+    const char* e = getenv("HG_SIG_W2");
+    return !e || atoi(e) != 0;
+  }();
+  return on && pad && n <= kSigW2MaxN;
+}
+void launch_sig_pairing_w2(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
+  if (n > 0) k_verify_sig_w2<<<nblk(n, 4), 128, 0, s>>>(sigs, flavor, n, tab, fe);
+}
 void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s,
-                        bool pad) {
+                        bool pad, bool allow_w2) {
   if (n <= 0) return;
   const int env = sig_env();
+  if (env < 0 && allow_w2 && sig_w2_for(pad, n)) {
+    launch_sig_pairing_w2(sigs, flavor, n, tab, fe, s);
+    return;
+  }
   if (env == 2) {
     k_verify_sig<2, true><<<nblk(n, 2), 32, 0, s>>>(nullptr, sigs, flavor, n, tab, nullptr, fe, nullptr);
     return;

@@ -49,7 +49,7 @@ HG_DEV void t12_unpark(const Team& T, int s, const uint32_t* park) {
     v[2 * i + 1] = x.y;
   }
   if (T.active) st_fp_a8(slot(T, s) + T.e * 10, v);
-  team_sync();
+  team_sync(T);
 }
 
 template <class P>

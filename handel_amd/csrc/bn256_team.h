@@ -28,6 +28,14 @@ struct Team {
   int k;           // Fp2 coefficient index e >> 1
   int comp;        // 0 = x (imag), 1 = y (real)
   bool active;     // tl < 12
+  // a team spread over the two waves of a workgroup (make_team_w2): lane tl
+  // of both waves owns element e; a round's products are split between the
+  // waves (bn256_xprog.h x_job_split) and team_sync is a workgroup barrier.
+  // Set from constants in every make_team*, so after inlining the branches on
+  // it fold away in the single-wave kernels.
+  bool split;
+  int wave;         // 0 or 1 (split teams)
+  uint32_t* xchg;   // split teams: this lane's 21 64-bit columns of wave 1's partial sum
 };
 
 HG_DEV uint32_t* slot(const Team& T, int s) { return T.base + s * kFp12Words; }
@@ -84,6 +92,12 @@ HG_DEV void team_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// team_sync for any team: a workgroup barrier when the team spans two waves
+HG_DEV void team_sync(const Team& T) {
+  if (T.split) __syncthreads();
+  else team_sync();
+}
+
 HG_DEV Team make_team(uint32_t* lds_base, int words_per_team) {
   Team T;
   int team = (threadIdx.x & 63) >> 4;  // teams are numbered within their wave
@@ -93,6 +107,23 @@ HG_DEV Team make_team(uint32_t* lds_base, int words_per_team) {
   T.e = T.active ? T.tl : 11;
   T.k = T.e >> 1;
   T.comp = T.e & 1;
+  T.split = false;
+  T.wave = 0;
+  T.xchg = nullptr;
+  return T;
+}
+
+// Four 16-lane teams over the two waves of a 128-thread workgroup: lane tl of
+// team t is lane 16 t + tl of BOTH waves; the pairing kernel's latency form
+// (bn256_gt.hip k_verify_sig_w2). xchg_base: 4 x 16 x kXchgWords words of LDS after
+// the teams' regions (wave 1's partial column sums, x_job_split).
+static constexpr int kXchgWords = 44;  // 21 64-bit columns, 16-byte aligned rows
+HG_DEV Team make_team_w2(uint32_t* lds_base, int words_per_team, uint32_t* xchg_base) {
+  Team T = make_team(lds_base, words_per_team);
+  const int team = (threadIdx.x & 63) >> 4;
+  T.split = true;
+  T.wave = threadIdx.x >> 6;
+  T.xchg = xchg_base + (team * 16 + T.tl) * kXchgWords;
   return T;
 }
 
@@ -114,6 +145,9 @@ HG_DEV Team make_team12(uint32_t* lds_base, int words_per_team) {
   T.e = T.active ? T.tl : 11;
   T.k = T.e >> 1;
   T.comp = T.e & 1;
+  T.split = false;
+  T.wave = 0;
+  T.xchg = nullptr;
   return T;
 }
 
@@ -218,9 +252,9 @@ HG_DEV void t12_mul(const Team& T, int dst, int sa, int sb) {
   }
   Fp r;
   acc_reduce_wide(r, acc);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
-  team_sync();
+  team_sync(T);
 }
 
 HG_DEV void t12_sqr(const Team& T, int dst, int sa) { t12_mul(T, dst, sa, sa); }
@@ -277,9 +311,9 @@ HG_DEV void t12_sqr_fast(const Team& T, int dst, int sa) {
   }
   Fp r;
   acc_reduce_wide(r, acc);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
-  team_sync();
+  team_sync(T);
 }
 
 // Granger-Scott squaring in the cyclotomic subgroup (valid after the easy part
@@ -340,9 +374,9 @@ HG_DEV void t12_cyc_sqr(const Team& T, int dst, int sa) {
   acc_add_shifted(acc, lin);
   Fp r;
   acc_reduce_wide(r, acc);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
-  team_sync();
+  team_sync(T);
 }
 
 // dst = a * (c + b w + a3 w^3) for line coefficients held in registers
@@ -367,9 +401,9 @@ HG_DEV void t12_mul_line(const Team& T, int dst, int sa, const Fp2& la, const Fp
   }
   Fp r;
   acc_reduce_wide(r, acc);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
-  team_sync();
+  team_sync(T);
 }
 
 // dst = conj_p6(a): negate odd powers of w (x/crypto gfP12.Conjugate)
@@ -378,9 +412,9 @@ HG_DEV void t12_conj(const Team& T, int dst, int sa) {
   ld_fp(v, slot(T, sa) + T.e * 10);
   fp_neg(n, v);
   fp_sel(v, (T.k & 1) != 0, n, v);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, v);
-  team_sync();
+  team_sync(T);
 }
 
 __constant__ static const Fp2 kGamma1[6] = HG_GAMMA1;
@@ -404,9 +438,9 @@ HG_DEV void t12_frob(const Team& T, int dst, int sa) {
   acc_mad(acc, u2, g.x);
   Fp r;
   acc_reduce(r, acc);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
-  team_sync();
+  team_sync(T);
 }
 
 // dst = a^(p^2) (gfP12.FrobeniusP2): coefficient k -> a_k * gamma2[k] (gamma2 in Fp)
@@ -416,9 +450,9 @@ HG_DEV void t12_frob2(const Team& T, int dst, int sa) {
   Fp g = kGamma2[T.k];
   Fp r;
   fp_mul(r, v, g);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, r);
-  team_sync();
+  team_sync(T);
 }
 
 HG_DEV void t12_set_one(const Team& T, int dst) {
@@ -428,15 +462,15 @@ HG_DEV void t12_set_one(const Team& T, int dst) {
   fp_one(one);
   fp_sel(v, T.e == 1, one, v);  // element 1 = c0.y
   if (T.active) st_fp(slot(T, dst) + T.e * 10, v);
-  team_sync();
+  team_sync(T);
 }
 
 HG_DEV void t12_copy(const Team& T, int dst, int sa) {
   Fp v;
   ld_fp(v, slot(T, sa) + T.e * 10);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(slot(T, dst) + T.e * 10, v);
-  team_sync();
+  team_sync(T);
 }
 
 // true (team-uniform) when slot s equals 1
@@ -482,12 +516,12 @@ HG_DEV void t12_inv_norm(const Team& T, int s2) {
   f2_sel(u, j == 1, xu, u);
   f2_sel(v, j == 0, xv, v);
   f2_sub(t, u, v);
-  team_sync();
+  team_sync(T);
   if (T.tl < 3) {  // odd coefficient 2j + 1 of s2
     st_fp(N + (4 * j + 2) * 10, t.x);
     st_fp(N + (4 * j + 3) * 10, t.y);
   }
-  team_sync();
+  team_sync(T);
   Fp2 t0, t1, t2;
   ld_f2(t0, N, 1);
   ld_f2(t1, N, 3);
@@ -497,12 +531,12 @@ HG_DEV void t12_inv_norm(const Team& T, int s2) {
   f2_sel(P, j == 0, c2, j == 1 ? c1 : c0);
   f2_sel(Q, j == 0, t1, j == 1 ? t2 : t0);
   f2_mul(w, P, Q);
-  team_sync();
+  team_sync(T);
   if (T.tl < 3) {
     st_fp(N + (4 * j + 2) * 10, w.x);
     st_fp(N + (4 * j + 3) * 10, w.y);
   }
-  team_sync();
+  team_sync(T);
   Fp2 w0, w1, w2, d;
   ld_f2(w0, N, 1);
   ld_f2(w1, N, 3);
@@ -528,9 +562,9 @@ HG_DEV void t12_inv_norm(const Team& T, int s2) {
   acc_reduce(e, acc);
   fp_zero(z);
   fp_sel(e, (T.k & 1) != 0, z, e);
-  team_sync();
+  team_sync(T);
   if (T.active) st_fp(N + T.e * 10, e);
-  team_sync();
+  team_sync(T);
 }
 
 // dst = a^-1 using scratch slots s1, s2 (x/crypto gfP12.Invert)

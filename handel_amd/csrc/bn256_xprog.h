@@ -307,6 +307,100 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
   else acc_reduce<FROM>(r, acc);                                  // products only: < 2p, one subtraction
 }
 
+// A single-job round on a team spread over two waves (Team::split): wave 0
+// sums products 0 .. H-1, wave 1 products H .. NP-1 and the linear terms and
+// hands its 21 columns to wave 0 through LDS (T.xchg, the same lane of the
+// other wave); wave 0 adds them and reduces. The column sums are those of
+// x_job, so the result is the same value. Ends with the round's closing
+// barrier.
+template <int W, int NP, int NL, int KL, int KS, int LZ, int EF>
+HG_DEV void x_job_split(const Team& T, const uint32_t (&w)[W], int base, Fp a0, Fp b0) {
+  constexpr int H = (NP + 1) / 2;  // wave 0's products
+  constexpr int H1 = NP - H;       // wave 1's
+  constexpr int lbase = 2 * NP;
+  uint64_t* X = reinterpret_cast<uint64_t*>(T.xchg);
+  if (T.wave != 0) {
+    if constexpr (H1 > 0 || NL > 0) {
+      Acc acc;
+      acc_zero(acc);
+      Fp lx[NL > 0 ? NL : 1];
+      if constexpr (NL > 0) x_for<NL>([&](auto t) { ld_fp_a8(lx[t], x_at(T, x_term_off(w, base + lbase + t))); });
+      Fp a, b;
+      if constexpr (H1 > 0) {
+        ld_fp_a8(a, x_at(T, x_off(w, base + 2 * H)));
+        ld_fp_a8(b, x_at(T, x_off(w, base + 2 * H + 1)));
+      }
+      if constexpr (NL > 0) {
+        uint32_t val[10];
+        x_lincomb_sum<W, NL, KL>(w, base + lbase, lx, val);
+#pragma unroll
+        for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] = val[l];
+      }
+      if constexpr (KS && H1 >= 3) x_products_ks<W, H1, false>(T, w, base + 2 * H, acc, a, b);
+      else if constexpr (H1 > 0) x_products<W, H1, false>(T, w, base + 2 * H, acc, a, b);
+      uint4* x4 = (uint4*)__builtin_assume_aligned(X, 16);
+#pragma unroll
+      for (int c = 0; c < 10; c++)
+        x4[c] = make_uint4((uint32_t)acc.c[2 * c], (uint32_t)(acc.c[2 * c] >> 32), (uint32_t)acc.c[2 * c + 1],
+                           (uint32_t)(acc.c[2 * c + 1] >> 32));
+      X[20] = acc.c[20];
+    }
+    __syncthreads();  // A: wave 1's columns in LDS, every read of wave 1 done
+    __syncthreads();  // the round's end
+    return;
+  }
+  Acc acc;
+  acc_zero(acc);
+  if constexpr (NP > 0 && !EF) {
+    ld_fp_a8(a0, x_at(T, x_off(w, base)));
+    ld_fp_a8(b0, x_at(T, x_off(w, base + 1)));
+  }
+  if constexpr (KS && H >= 3) x_products_ks<W, H, false>(T, w, base, acc, a0, b0);
+  else x_products<W, H, false>(T, w, base, acc, a0, b0);
+  const uint32_t dst = x_off(w, base + lbase + NL);
+  __syncthreads();  // A
+  if constexpr (H1 > 0 || NL > 0) {
+    const uint4* x4 = (const uint4*)__builtin_assume_aligned(X, 16);
+#pragma unroll
+    for (int c = 0; c < 10; c++) {
+      const uint4 v = x4[c];
+      acc.c[2 * c] += (uint64_t)v.x | ((uint64_t)v.y << 32);
+      acc.c[2 * c + 1] += (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+    acc.c[20] += X[20];
+  }
+  Fp r;
+  if constexpr (NL > 0 && LZ) acc_reduce_wide_lazy<0>(r, acc);
+  else if constexpr (NL > 0) acc_reduce_wide<0>(r, acc);
+  else acc_reduce<0>(r, acc);
+  if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
+  __syncthreads();  // the round's end
+}
+
+// the pre-pass of a split team's round: values v = T.wave, T.wave + 2, ...
+template <int NV, int NT, int W, int KP>
+HG_DEV void x_prepass_split(const Team& T, const uint32_t (&w)[W]) {
+  auto half = [&](auto par) {
+    constexpr int P = decltype(par)::value;
+    constexpr int NH = (NV - P + 1) / 2;  // values P, P + 2, ...
+    if constexpr (NH > 0) {
+      Fp xs[NH][NT];
+      x_for<NH>([&](auto h) {
+        x_for<NT>([&](auto t) { ld_fp_a8(xs[h][t], x_at(T, x_term_off(w, (P + 2 * h) * (1 + NT) + 1 + t))); });
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t val[NH][10];
+      x_for<NH>([&](auto h) { x_lincomb_sum<W, NT, KP>(w, (P + 2 * h) * (1 + NT) + 1, xs[h], val[h]); });
+      x_for<NH>([&](auto h) {
+        const uint32_t dst = x_off(w, (P + 2 * h) * (1 + NT));
+        if (dst != 0xffffu) st_fp_a8(x_at(T, dst), val[h]);
+      });
+    }
+  };
+  if (T.wave == 0) half(std::integral_constant<int, 0>{});
+  else half(std::integral_constant<int, 1>{});
+}
+
 // One round. Table layout per lane (16-bit entries): NV x (dst, NT x term),
 // then job 1 (NP x (u, v), NL x term, dst) and, in a fused round (NP2 + NL2 >
 // 0), job 2 (NP2 x (u, v), NL2 x term, dst2); padded to W dwords. Both jobs
@@ -334,6 +428,10 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     // the values are pinned before the first store, so the compiler cannot
     // sink a combination into its store's branch: the loads of all
     // combinations issue together instead of one LDS latency per combination
+    if (T.split) {  // a split team: wave w evaluates the values v = w mod 2
+      x_prepass_split<NV, NT, W, KP>(T, w);
+      team_sync(T);
+    } else {
     Fp xs[NV][NT];
     x_for<NV>([&](auto v) {
       x_for<NT>([&](auto t) { ld_fp_a8(xs[v][t], x_at(T, x_term_off(w, v * (1 + NT) + 1 + t))); });
@@ -350,6 +448,13 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
       if (dst != 0xffffu) st_fp_a8(x_at(T, dst), val[v]);
     });
     team_sync();
+    }
+  }
+  if constexpr (NP2 == 0 && NL2 == 0) {
+    if (T.split) {
+      x_job_split<W, NP, NL, KL1, KS1, LZ, EF>(T, w, jbase, e0, e1);
+      return;
+    }
   }
   Fp r;
   uint32_t dst;
@@ -359,14 +464,17 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     Fp r2;
     uint32_t dst2;
     x_job<W, NP2, NL2, KL2, KS2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
-    team_sync();
-    if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
-    if (dst2 != 0xffffu) st_fp_a8(x_at(T, dst2), r2.l);
+    team_sync(T);
+    // a split team runs a fused round whole on both waves; wave 0 stores
+    if (!T.split || T.wave == 0) {
+      if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
+      if (dst2 != 0xffffu) st_fp_a8(x_at(T, dst2), r2.l);
+    }
   } else {
-    team_sync();
+    team_sync(T);
     if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
   }
-  team_sync();
+  team_sync(T);
 }
 
 // ------------------------------------------------------------------ call-site wrappers

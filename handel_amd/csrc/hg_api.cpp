@@ -915,7 +915,11 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
         launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)ws.sig_lines.p, ws.gt_fe.p, s,
                              lane ? lane->pad : true);
       else
-        launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s, lane ? lane->pad : true);
+        // the two-wave latency form only for the context's own submissions
+        // (one batch at a time); lanes keep batches in flight, where twice the
+        // waves per check costs throughput
+        launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s, lane ? lane->pad : true,
+                           lane == nullptr);
       t.stop();
       HG_CHECK(c, hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
       launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, ws.pts1.p, d_codes, (int*)gw.hdr,
@@ -1547,7 +1551,7 @@ int hg_debug_fp12(hg_ctx* c, int op, const uint8_t* a, const uint8_t* b, size_t 
 }
 
 int hg_sig_pairing_device(hg_ctx* c, const uint8_t* d_sigs, size_t n, uint8_t* d_fe, int kernel, void* stream) {
-  if (!c || (n && (!d_sigs || !d_fe)) || n > (size_t)INT32_MAX || kernel < 0 || kernel > 3) return HG_ERR_ARG;
+  if (!c || (n && (!d_sigs || !d_fe)) || n > (size_t)INT32_MAX || kernel < 0 || kernel > 4) return HG_ERR_ARG;
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
@@ -1555,11 +1559,13 @@ int hg_sig_pairing_device(hg_ctx* c, const uint8_t* d_sigs, size_t n, uint8_t* d
   Submission sub(c, s);
   HG_CHECK(c, sub.start());
   const bool pad = (kernel & 1) == 0;
-  if (kernel >= 2) {
+  if (kernel == 4) {
+    launch_sig_pairing_w2(d_sigs, c->flavor, (int)n, c->d_lines, (Gt*)d_fe, s);
+  } else if (kernel >= 2) {
     HG_CHECK(c, c->ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
     launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)c->ws.sig_lines.p, (Gt*)d_fe, s, pad);
   } else {
-    launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, (Gt*)d_fe, s, pad);
+    launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, (Gt*)d_fe, s, pad, false);
   }
   int rc = check_launch(c);
   if (rc) return rc;

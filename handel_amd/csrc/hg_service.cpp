@@ -314,13 +314,15 @@ void hg_service::finish_slots(const Pending* items, size_t n, const int32_t* cod
 
 void hg_service::complete(int lane, const int32_t* codes, int32_t fail) {
   LaneState& L = lanes[lane];
+  // the counters first: a client that sees its verdict (the tail's release
+  // store in finish_slots) sees them counted
+  v.h->batches.fetch_add(1, std::memory_order_relaxed);
+  v.h->requests.fetch_add(L.slots.size(), std::memory_order_relaxed);
   finish_slots(L.slots.data(), L.slots.size(), codes, fail);
   for (const Pending& p : L.slots)
     if (p.chan < released.size()) released[p.chan]++;
   returning += L.slots.size();
   released_any = true;
-  v.h->batches.fetch_add(1, std::memory_order_relaxed);
-  v.h->requests.fetch_add(L.slots.size(), std::memory_order_relaxed);
   L.slots.clear();
   L.busy = false;
   busy--;

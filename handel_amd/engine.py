@@ -168,7 +168,7 @@ class Engine:
                     "hg_pack_verdicts_device")
 
     # hg_sig_pairing_device kernels
-    SIG_K16_PAD, SIG_K16, SIG_K12_PAD, SIG_K12 = 0, 1, 2, 3
+    SIG_K16_PAD, SIG_K16, SIG_K12_PAD, SIG_K12, SIG_W2 = 0, 1, 2, 3, 4
 
     def sig_pairing_device(self, d_sigs: int, n: int, d_fe: int, kernel: int, stream: int = 0):
         """FE(Miller(G2Base at -sig)) of n signature marshals into d_fe (n x 480

@@ -155,7 +155,7 @@ print(json.dumps({"codes": [int(c) for c in codes], "level": e.aggregate_tables(
 
 
 def _child(env_over, code=_CHILD):
-    env = {k: v for k, v in os.environ.items() if k not in ("HG_GT_LEVEL", "HG_AGG_PATH", "HG_SIG12")}
+    env = {k: v for k, v in os.environ.items() if k not in ("HG_GT_LEVEL", "HG_AGG_PATH", "HG_SIG12", "HG_SIG_W2")}
     env.update(env_over)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -175,12 +175,15 @@ def test_gt_and_g2_paths_agree():
             ("gt16c16", {"HG_GT_LEVEL": "2", "HG_GT_CHUNK": "16"}),
             ("gt16c5", {"HG_GT_LEVEL": "2", "HG_GT_CHUNK": "5"}),
             # the signature pairing on 12-lane teams (bn256_sig12.hip) on the
-            # padded context path too, and the 16-lane kernel everywhere
+            # padded context path too, and the 16-lane kernel everywhere (the
+            # 1024-check batch: two-wave teams, k_verify_sig_w2, unless
+            # HG_SIG_W2=0)
             ("gt16sig12", {"HG_GT_LEVEL": "2", "HG_SIG12": "1"}),
-            ("gt16sig16", {"HG_GT_LEVEL": "2", "HG_SIG12": "0"}))
+            ("gt16sig16", {"HG_GT_LEVEL": "2", "HG_SIG12": "0"}),
+            ("gt16w1", {"HG_GT_LEVEL": "2", "HG_SIG12": "0", "HG_SIG_W2": "0"}))
     for name, env in runs:
         outs[name] = _child(env)
-    assert [outs[k]["level"] for k, _ in runs] == [2, 1, 0, 0, 2, 2, 2, 2]
+    assert [outs[k]["level"] for k, _ in runs] == [2, 1, 0, 0, 2, 2, 2, 2, 2]
     assert all(outs[k]["codes"] == outs["gt16"]["codes"] for k, _ in runs)
     import bench
     from handel_amd.engine import Engine

@@ -161,7 +161,7 @@ def test_headline_lanes_match_oracle_committee(request, flavor):
 def test_pairing_kernels_give_identical_fe_values(engine, engine_cf):
     """hg_sig_pairing_device: the 16-lane k_verify_sig (padded, unpadded) and
     the 12-lane k_verify_sig12 (padded, unpadded, with k_sig_scalars /
-    k_sig_lines) write byte-identical FE(Miller(G2Base at -sig)) values for
+    k_sig_lines) and the two-wave k_verify_sig_w2 write byte-identical FE(Miller(G2Base at -sig)) values for
     valid signatures and the point at infinity, ragged n (teams of the last
     wave partly empty), both flavors. The verdict tests pin those values to
     the oracle through the comparison with the fold."""
@@ -178,14 +178,14 @@ def test_pairing_kernels_give_identical_fe_values(engine, engine_cf):
             sigs[0:64] = bytes(64)  # the point at infinity
             d_sigs = bench._dev_bytes(bytes(sigs), dev)
             outs = []
-            for k in range(4):
+            for k in range(5):
                 fe = torch.full((n * 480,), 0x5A, dtype=torch.uint8, device=dev)
                 # (torch's default stream is handle 0: the context's own stream runs it)
                 eng.sig_pairing_device(d_sigs.data_ptr(), n, fe.data_ptr(), k,
                                        torch.cuda.current_stream(dev).cuda_stream)
                 torch.cuda.synchronize(dev)
                 outs.append(fe.cpu().numpy())
-            for k in range(1, 4):
+            for k in range(1, 5):
                 assert np.array_equal(outs[0], outs[k]), (eng.flavor_name, n, k)
             # e(inf, G2Base) = 1: the first value is the GT identity (only
             # element 1, c0.y, nonzero: one in Montgomery form)

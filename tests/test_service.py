@@ -271,10 +271,14 @@ def test_client_rewriting_its_queued_slot_cannot_change_the_batch(new_bitlen):
             w = np.array([0x1234_5678_9abc_def0], dtype=np.uint64)
             t = cl.submit(MSG, 64, 64, 64, w, echo_signature(w))
             t_bad = cl.submit(MSG, 64, 64, 64, w, echo_signature(w, True))
-            time.sleep(0.05)  # taken by the dispatcher, not launched (300 ms linger)
             big = slot_words * 64 if new_bitlen == "max" else 0xFFFFFFFF
             for tk in (t, t_bad):
                 base = slot_at(tk & 0xFFFFFFFF)
+                # taken by the dispatcher, not launched (300 ms linger); polled,
+                # so a loaded machine's slow dispatcher wake-up is no failure
+                t0 = time.time()
+                while struct.unpack_from("<I", m, base)[0] != 3 and time.time() - t0 < 0.25:
+                    time.sleep(0.002)
                 state = struct.unpack_from("<I", m, base)[0]
                 assert state == 3, "the slot is Taken (kSlotTaken) while it lingers"
                 struct.pack_into("<III", m, base + 24, 0, big, big)  # offset, bitlen, level_size
