@@ -67,12 +67,15 @@ void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt
 // the same check in two launches, so the fold can run beside the pairing:
 // fe[r] = FE(Miller(G2Base at -sig_r)) from the 64-byte marshals (decoded in
 // the kernel), then fe[r] == y[r] where still HG_OK
-// k_verify_sig_w2: a check's team spread over two waves (latency form); the
-// padded launch_sig_pairing takes it for n <= 2048 unless HG_SIG_W2=0
-bool sig_w2_for(bool pad, int n);
+// k_verify_sig_w2: a check's team spread over two waves (latency form); a
+// padded launch_sig_pairing takes it for n <= min(w2_max, 2048) unless
+// HG_SIG_W2=0. sig_w2_lane_max: the bound for lanes (HG_SIG_W2_LANE_MAX, 0)
+static constexpr int kSigW2MaxN = 2048;
+bool sig_w2_for(bool pad, int n, int w2_max);
+int sig_w2_lane_max();
 void launch_sig_pairing_w2(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s);
 void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s,
-                        bool pad = true, bool allow_w2 = true);
+                        bool pad = true, int w2_max = kSigW2MaxN);
 // launch_sig_pairing on five 12-lane teams per wave (bn256_sig12.hip): the
 // lines evaluated at -sig first (k_sig_lines, into ev: sig12_lines_bytes(n)),
 // then k_verify_sig12; the same fe values

@@ -698,7 +698,6 @@ __global__ __launch_bounds__(64) void k_verify_sig(const PointG1* sigs, const ui
 // chain is about half as long for the same values. Twice the waves per check:
 // it pays when the batch is small (n <= kSigW2MaxN: 2n waves still fit one per
 // SIMD) and the step waits on the pairing — a lone batch's latency.
-static constexpr int kSigW2MaxN = 2048;
 __global__ __launch_bounds__(128) void k_verify_sig_w2(const uint8_t* sig_bytes, int flavor, int n,
                                                        const LineCoef* tab, Gt* fe) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * kSigTeamWords + 4 * 16 * kXchgWords];
@@ -811,23 +810,30 @@ static int sig_env() {
   }();
   return v;
 }
-// the two-wave teams for a padded launch of at most kSigW2MaxN checks;
-// HG_SIG_W2=0 turns them off (A/B)
-bool sig_w2_for(bool pad, int n) {
+// the two-wave teams for a padded launch of at most w2_max (<= kSigW2MaxN)
+// checks; HG_SIG_W2=0 turns them off (A/B)
+bool sig_w2_for(bool pad, int n, int w2_max) {
   static const bool on = [] {
     const char* e = getenv("HG_SIG_W2");
     return !e || atoi(e) != 0;
   }();
-  return on && pad && n <= kSigW2MaxN;
+  return on && pad && n <= w2_max && n <= kSigW2MaxN;
+}
+int sig_w2_lane_max() {
+  static const int v = [] {
+    const char* e = getenv("HG_SIG_W2_LANE_MAX");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 void launch_sig_pairing_w2(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s) {
   if (n > 0) k_verify_sig_w2<<<nblk(n, 4), 128, 0, s>>>(sigs, flavor, n, tab, fe);
 }
 void launch_sig_pairing(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Gt* fe, hipStream_t s,
-                        bool pad, bool allow_w2) {
+                        bool pad, int w2_max) {
   if (n <= 0) return;
   const int env = sig_env();
-  if (env < 0 && allow_w2 && sig_w2_for(pad, n)) {
+  if (env < 0 && sig_w2_for(pad, n, w2_max)) {
     launch_sig_pairing_w2(sigs, flavor, n, tab, fe, s);
     return;
   }

@@ -915,11 +915,11 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
         launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)ws.sig_lines.p, ws.gt_fe.p, s,
                              lane ? lane->pad : true);
       else
-        // the two-wave latency form only for the context's own submissions
-        // (one batch at a time); lanes keep batches in flight, where twice the
-        // waves per check costs throughput
+        // the two-wave latency form for the context's own submissions (one
+        // batch at a time); lanes keep batches in flight, where twice the
+        // waves per check costs throughput (HG_SIG_W2_LANE_MAX: A/B)
         launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s, lane ? lane->pad : true,
-                           lane == nullptr);
+                           lane ? sig_w2_lane_max() : kSigW2MaxN);
       t.stop();
       HG_CHECK(c, hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
       launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, ws.pts1.p, d_codes, (int*)gw.hdr,
@@ -1565,7 +1565,7 @@ int hg_sig_pairing_device(hg_ctx* c, const uint8_t* d_sigs, size_t n, uint8_t* d
     HG_CHECK(c, c->ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
     launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)c->ws.sig_lines.p, (Gt*)d_fe, s, pad);
   } else {
-    launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, (Gt*)d_fe, s, pad, false);
+    launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, (Gt*)d_fe, s, pad, 0);
   }
   int rc = check_launch(c);
   if (rc) return rc;
