@@ -92,9 +92,17 @@ HG_DEV void team_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Split teams exist only in translation units that define HG_TEAM_SPLIT 1
+// before their includes (bn256_sigw2.hip): everywhere else every branch on
+// Team::split is compiled out, so the one-wave kernels' code is untouched.
+#ifndef HG_TEAM_SPLIT
+#define HG_TEAM_SPLIT 0
+#endif
+static constexpr bool kTeamSplit = HG_TEAM_SPLIT != 0;
+
 // team_sync for any team: a workgroup barrier when the team spans two waves
 HG_DEV void team_sync(const Team& T) {
-  if (T.split) __syncthreads();
+  if (kTeamSplit && T.split) __syncthreads();
   else team_sync();
 }
 

@@ -428,7 +428,7 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     // the values are pinned before the first store, so the compiler cannot
     // sink a combination into its store's branch: the loads of all
     // combinations issue together instead of one LDS latency per combination
-    if (T.split) {  // a split team: wave w evaluates the values v = w mod 2
+    if (kTeamSplit && T.split) {  // a split team: wave w evaluates the values v = w mod 2
       x_prepass_split<NV, NT, W, KP>(T, w);
       team_sync(T);
     } else {
@@ -450,7 +450,7 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     team_sync();
     }
   }
-  if constexpr (NP2 == 0 && NL2 == 0) {
+  if constexpr (kTeamSplit && NP2 == 0 && NL2 == 0) {
     if (T.split) {
       x_job_split<W, NP, NL, KL1, KS1, LZ, EF>(T, w, jbase, e0, e1);
       return;
@@ -466,7 +466,7 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     x_job<W, NP2, NL2, KL2, KS2>(T, w, jbase + 2 * NP + NL + 1, r2, dst2);
     team_sync(T);
     // a split team runs a fused round whole on both waves; wave 0 stores
-    if (!T.split || T.wave == 0) {
+    if (!kTeamSplit || !T.split || T.wave == 0) {
       if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
       if (dst2 != 0xffffu) st_fp_a8(x_at(T, dst2), r2.l);
     }

@@ -33,6 +33,30 @@ def bundles(path):
         pos = i + 1
 
 
+def resources(path):
+    """{kernel symbol: {"vgpr", "vgpr_spill", "sgpr_spill", "lds", "scratch"}} from
+    the gfx950 code objects' metadata notes (llvm-readelf --notes)."""
+    import re
+
+    out = {}
+    for triple, blob in bundles(path):
+        if "gfx950" not in triple:
+            continue
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(blob)
+            f.flush()
+            notes = subprocess.run([LLVM + "llvm-readelf", "--notes", f.name], capture_output=True, text=True).stdout
+        for b in notes.split("- .agpr_count")[1:]:
+            def g(k):
+                m = re.search(r"\." + k + r":\s+(\S+)", b)
+                return int(m.group(1)) if m else None
+            name = re.search(r"\.name:\s+(\S+)", b).group(1)
+            out[name] = {"vgpr": g("vgpr_count"), "vgpr_spill": g("vgpr_spill_count"),
+                         "sgpr_spill": g("sgpr_spill_count"), "lds": g("group_segment_fixed_size"),
+                         "scratch": g("private_segment_fixed_size")}
+    return out
+
+
 def main():
     for triple, blob in bundles(sys.argv[1]):
         with tempfile.NamedTemporaryFile(suffix=".co") as f:
