@@ -22,7 +22,7 @@ DIAG_LIB = os.path.join(OUT_DIR, "libhandel_gpu_diag.so")
 SOURCES = ["bn256_verify.hip", "bn256_pair.hip", "bn256_kernels.hip", "bn256_gt.hip", "bn256_sig12.hip", "bn256_sigw2.hip", "hg_api.cpp",
            "hg_batcher.cpp", "hg_packets.hip", "hg_service.cpp"]
 HEADERS = ["bn256_fp.h", "bn256_curve.h", "bn256_team.h", "bn256_kernels.h", "bn256_constants.h",
-           "bn256_g2team.h", "bn256_g2sched.h", "bn256_pairing.h", "bn256_xprog.h", "bn256_xtab.h", "bn256_inv.h", "bn256_agg.h", "bn256_gt.h", "bn256_decode.h", "hg_packets.h", "hg_shm.h", "hg_codes.h", "bn256_sigfe.h", "bn256_sigteam.h"]
+           "bn256_g2team.h", "bn256_g2sched.h", "bn256_pairing.h", "bn256_xprog.h", "bn256_xtab.h", "bn256_inv.h", "bn256_agg.h", "bn256_gt.h", "bn256_decode.h", "hg_packets.h", "hg_shm.h", "hg_codes.h", "bn256_sigfe.h", "bn256_sigteam.h", "bn256_sigsplit.h"]
 ARCH = os.environ.get("HG_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]

@@ -67,9 +67,10 @@ void launch_verify_sig(const PointG1* sigs, int n, const LineCoef* tab, const Gt
 // the same check in two launches, so the fold can run beside the pairing:
 // fe[r] = FE(Miller(G2Base at -sig_r)) from the 64-byte marshals (decoded in
 // the kernel), then fe[r] == y[r] where still HG_OK
-// k_verify_sig_w2: a check's team spread over two waves (latency form); a
-// padded launch_sig_pairing takes it for n <= min(w2_max, 2048) unless
-// HG_SIG_W2=0. sig_w2_lane_max: the bound for lanes (HG_SIG_W2_LANE_MAX, 0)
+// k_verify_sig_split<2>: a check's team spread over two waves (the latency
+// form, bn256_sigsplit.h); a padded launch_sig_pairing of n <= min(w2_max,
+// 2048) checks takes it unless HG_SIG_W2=0. sig_w2_lane_max: the bound for
+// lanes (HG_SIG_W2_LANE_MAX, 0)
 static constexpr int kSigW2MaxN = 2048;
 bool sig_w2_for(bool pad, int n, int w2_max);
 int sig_w2_lane_max();

@@ -2,7 +2,7 @@
 // both of its 16-lane kernels use: GT values between HBM and team slots, the
 // Miller loop at -sig (G2Base lines from the table), the layout-S team region.
 // k_verify_sig (bn256_gt.hip) runs them on one wave per team, the latency form
-// k_verify_sig_w2 (bn256_sigw2.hip) on teams spread over two waves.
+// k_verify_sig_split (bn256_sigsplit.h) on teams spread over 2 or 4 waves.
 #pragma once
 
 #include "bn256_gt.h"

@@ -28,14 +28,14 @@ struct Team {
   int k;           // Fp2 coefficient index e >> 1
   int comp;        // 0 = x (imag), 1 = y (real)
   bool active;     // tl < 12
-  // a team spread over the two waves of a workgroup (make_team_w2): lane tl
-  // of both waves owns element e; a round's products are split between the
-  // waves (bn256_xprog.h x_job_split) and team_sync is a workgroup barrier.
-  // Set from constants in every make_team*, so after inlining the branches on
-  // it fold away in the single-wave kernels.
+  // a team spread over the kSplitWaves waves of a workgroup
+  // (make_team_split): lane tl of every wave owns element e; a round's
+  // products are split between the waves (bn256_xprog.h x_job_split) and
+  // team_sync is a workgroup barrier. Only units built with HG_TEAM_SPLIT
+  // (below) look at these fields.
   bool split;
-  int wave;         // 0 or 1 (split teams)
-  uint32_t* xchg;   // split teams: this lane's 21 64-bit columns of wave 1's partial sum
+  int wave;         // the wave within the workgroup (split teams)
+  uint32_t* xchg;   // split teams: this lane's partial-column rows (kXchgWords words per other wave)
 };
 
 HG_DEV uint32_t* slot(const Team& T, int s) { return T.base + s * kFp12Words; }
@@ -92,13 +92,14 @@ HG_DEV void team_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Split teams exist only in translation units that define HG_TEAM_SPLIT 1
-// before their includes (bn256_sigw2.hip): everywhere else every branch on
-// Team::split is compiled out, so the one-wave kernels' code is untouched.
+// Split teams exist only in translation units that define HG_TEAM_SPLIT (the
+// waves per team) before their includes (bn256_sigw2.hip): everywhere else every branch on Team::split is compiled
+// out, so the one-wave kernels' code is untouched.
 #ifndef HG_TEAM_SPLIT
 #define HG_TEAM_SPLIT 0
 #endif
-static constexpr bool kTeamSplit = HG_TEAM_SPLIT != 0;
+static constexpr bool kTeamSplit = HG_TEAM_SPLIT > 1;
+static constexpr int kSplitWaves = HG_TEAM_SPLIT > 1 ? HG_TEAM_SPLIT : 1;
 
 // team_sync for any team: a workgroup barrier when the team spans two waves
 HG_DEV void team_sync(const Team& T) {
@@ -121,17 +122,18 @@ HG_DEV Team make_team(uint32_t* lds_base, int words_per_team) {
   return T;
 }
 
-// Four 16-lane teams over the two waves of a 128-thread workgroup: lane tl of
-// team t is lane 16 t + tl of BOTH waves; the pairing kernel's latency form
-// (bn256_gt.hip k_verify_sig_w2). xchg_base: 4 x 16 x kXchgWords words of LDS after
-// the teams' regions (wave 1's partial column sums, x_job_split).
+// Four 16-lane teams over the kSplitWaves waves of a workgroup: lane tl of
+// team t is lane 16 t + tl of EVERY wave; the pairing kernel's latency forms
+// (bn256_sigsplit.h). xchg_base: 4 x 16 x (kSplitWaves - 1) x kXchgWords words
+// of LDS after the teams' regions (the other waves' partial column sums,
+// bn256_xprog.h x_job_split).
 static constexpr int kXchgWords = 44;  // 21 64-bit columns, 16-byte aligned rows
-HG_DEV Team make_team_w2(uint32_t* lds_base, int words_per_team, uint32_t* xchg_base) {
+HG_DEV Team make_team_split(uint32_t* lds_base, int words_per_team, uint32_t* xchg_base) {
   Team T = make_team(lds_base, words_per_team);
   const int team = (threadIdx.x & 63) >> 4;
   T.split = true;
   T.wave = threadIdx.x >> 6;
-  T.xchg = xchg_base + (team * 16 + T.tl) * kXchgWords;
+  T.xchg = xchg_base + (team * 16 + T.tl) * (kSplitWaves - 1) * kXchgWords;
   return T;
 }
 

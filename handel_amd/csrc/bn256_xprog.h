@@ -307,68 +307,95 @@ HG_DEV void x_job(const Team& T, const uint32_t (&w)[W], int base, Fp& r, uint32
   else acc_reduce<FROM>(r, acc);                                  // products only: < 2p, one subtraction
 }
 
-// A single-job round on a team spread over two waves (Team::split): wave 0
-// sums products 0 .. H-1, wave 1 products H .. NP-1 and the linear terms and
-// hands its 21 columns to wave 0 through LDS (T.xchg, the same lane of the
-// other wave); wave 0 adds them and reduces. The column sums are those of
-// x_job, so the result is the same value. Ends with the round's closing
+// A single-job round on a team spread over the kSplitWaves waves of a
+// workgroup (Team::split): the products are cut into kSplitWaves contiguous
+// ranges, wave r sums range r, the last wave also the linear terms; waves
+// 1.. hand their 21 columns to wave 0 through LDS (T.xchg, the same lane of
+// the other waves), wave 0 adds them and reduces. The column sums are those
+// of x_job, so the result is the same value. Ends with the round's closing
 // barrier.
+template <int NP, int R>
+struct XSplitRange {
+  static constexpr int kQ = (NP + kSplitWaves - 1) / kSplitWaves;
+  static constexpr int kLo = R * kQ < NP ? R * kQ : NP;
+  static constexpr int kHi = (R + 1) * kQ < NP ? (R + 1) * kQ : NP;
+  static constexpr int kN = kHi - kLo;
+};
 template <int W, int NP, int NL, int KL, int KS, int LZ, int EF>
 HG_DEV void x_job_split(const Team& T, const uint32_t (&w)[W], int base, Fp a0, Fp b0) {
-  constexpr int H = (NP + 1) / 2;  // wave 0's products
-  constexpr int H1 = NP - H;       // wave 1's
   constexpr int lbase = 2 * NP;
-  uint64_t* X = reinterpret_cast<uint64_t*>(T.xchg);
-  if (T.wave != 0) {
-    if constexpr (H1 > 0 || NL > 0) {
+  constexpr int H = XSplitRange<NP, 0>::kN;  // wave 0's products
+  // wave r > 0: its partial columns, if it has any work
+  auto partial = [&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    using Rg = XSplitRange<NP, R>;
+    constexpr bool kLin = R == kSplitWaves - 1 && NL > 0;
+    if constexpr (Rg::kN > 0 || kLin) {
       Acc acc;
       acc_zero(acc);
       Fp lx[NL > 0 ? NL : 1];
-      if constexpr (NL > 0) x_for<NL>([&](auto t) { ld_fp_a8(lx[t], x_at(T, x_term_off(w, base + lbase + t))); });
+      if constexpr (kLin) x_for<NL>([&](auto t) { ld_fp_a8(lx[t], x_at(T, x_term_off(w, base + lbase + t))); });
       Fp a, b;
-      if constexpr (H1 > 0) {
-        ld_fp_a8(a, x_at(T, x_off(w, base + 2 * H)));
-        ld_fp_a8(b, x_at(T, x_off(w, base + 2 * H + 1)));
+      if constexpr (Rg::kN > 0) {
+        ld_fp_a8(a, x_at(T, x_off(w, base + 2 * Rg::kLo)));
+        ld_fp_a8(b, x_at(T, x_off(w, base + 2 * Rg::kLo + 1)));
       }
-      if constexpr (NL > 0) {
-        uint32_t val[10];
-        x_lincomb_sum<W, NL, KL>(w, base + lbase, lx, val);
+      if constexpr (NL > 0) {  // (NL first: the call below does not depend on R)
+        if constexpr (kLin) {
+          uint32_t val[10];
+          x_lincomb_sum<W, NL, KL>(w, base + lbase, lx, val);
 #pragma unroll
-        for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] = val[l];
+          for (int l = 0; l < 10; l++) acc.c[kRedcSteps + l] = val[l];
+        }
       }
-      if constexpr (KS && H1 >= 3) x_products_ks<W, H1, false>(T, w, base + 2 * H, acc, a, b);
-      else if constexpr (H1 > 0) x_products<W, H1, false>(T, w, base + 2 * H, acc, a, b);
-      uint4* x4 = (uint4*)__builtin_assume_aligned(X, 16);
+      if constexpr (KS && Rg::kN >= 3) x_products_ks<W, Rg::kN, false>(T, w, base + 2 * Rg::kLo, acc, a, b);
+      else if constexpr (Rg::kN > 0) x_products<W, Rg::kN, false>(T, w, base + 2 * Rg::kLo, acc, a, b);
+      uint4* x4 = (uint4*)__builtin_assume_aligned(T.xchg + (R - 1) * kXchgWords, 16);
 #pragma unroll
       for (int c = 0; c < 10; c++)
         x4[c] = make_uint4((uint32_t)acc.c[2 * c], (uint32_t)(acc.c[2 * c] >> 32), (uint32_t)acc.c[2 * c + 1],
                            (uint32_t)(acc.c[2 * c + 1] >> 32));
-      X[20] = acc.c[20];
+      reinterpret_cast<uint64_t*>(T.xchg + (R - 1) * kXchgWords)[20] = acc.c[20];
     }
-    __syncthreads();  // A: wave 1's columns in LDS, every read of wave 1 done
+  };
+  if (T.wave != 0) {
+    if constexpr (kSplitWaves == 2) {
+      partial(std::integral_constant<int, 1>{});
+    } else {
+      x_for<kSplitWaves - 1>([&](auto r) {
+        constexpr int R = decltype(r)::value + 1;
+        if (T.wave == R) partial(std::integral_constant<int, R>{});
+      });
+    }
+    __syncthreads();  // A: the partial columns in LDS, every read of these waves done
     __syncthreads();  // the round's end
     return;
   }
   Acc acc;
   acc_zero(acc);
-  if constexpr (NP > 0 && !EF) {
-    ld_fp_a8(a0, x_at(T, x_off(w, base)));
-    ld_fp_a8(b0, x_at(T, x_off(w, base + 1)));
+  if constexpr (H > 0) {
+    if constexpr (!EF) {
+      ld_fp_a8(a0, x_at(T, x_off(w, base)));
+      ld_fp_a8(b0, x_at(T, x_off(w, base + 1)));
+    }
+    if constexpr (KS && H >= 3) x_products_ks<W, H, false>(T, w, base, acc, a0, b0);
+    else x_products<W, H, false>(T, w, base, acc, a0, b0);
   }
-  if constexpr (KS && H >= 3) x_products_ks<W, H, false>(T, w, base, acc, a0, b0);
-  else x_products<W, H, false>(T, w, base, acc, a0, b0);
   const uint32_t dst = x_off(w, base + lbase + NL);
   __syncthreads();  // A
-  if constexpr (H1 > 0 || NL > 0) {
-    const uint4* x4 = (const uint4*)__builtin_assume_aligned(X, 16);
+  x_for<kSplitWaves - 1>([&](auto r) {
+    constexpr int R = decltype(r)::value + 1;
+    if constexpr (XSplitRange<NP, R>::kN > 0 || (R == kSplitWaves - 1 && NL > 0)) {
+      const uint4* x4 = (const uint4*)__builtin_assume_aligned(T.xchg + (R - 1) * kXchgWords, 16);
 #pragma unroll
-    for (int c = 0; c < 10; c++) {
-      const uint4 v = x4[c];
-      acc.c[2 * c] += (uint64_t)v.x | ((uint64_t)v.y << 32);
-      acc.c[2 * c + 1] += (uint64_t)v.z | ((uint64_t)v.w << 32);
+      for (int c = 0; c < 10; c++) {
+        const uint4 v = x4[c];
+        acc.c[2 * c] += (uint64_t)v.x | ((uint64_t)v.y << 32);
+        acc.c[2 * c + 1] += (uint64_t)v.z | ((uint64_t)v.w << 32);
+      }
+      acc.c[20] += reinterpret_cast<const uint64_t*>(T.xchg + (R - 1) * kXchgWords)[20];
     }
-    acc.c[20] += X[20];
-  }
+  });
   Fp r;
   if constexpr (NL > 0 && LZ) acc_reduce_wide_lazy<0>(r, acc);
   else if constexpr (NL > 0) acc_reduce_wide<0>(r, acc);
@@ -377,28 +404,37 @@ HG_DEV void x_job_split(const Team& T, const uint32_t (&w)[W], int base, Fp a0, 
   __syncthreads();  // the round's end
 }
 
-// the pre-pass of a split team's round: values v = T.wave, T.wave + 2, ...
+// the pre-pass of a split team's round: wave r evaluates the values v = r,
+// r + kSplitWaves, ...
 template <int NV, int NT, int W, int KP>
 HG_DEV void x_prepass_split(const Team& T, const uint32_t (&w)[W]) {
-  auto half = [&](auto par) {
+  auto part = [&](auto par) {
     constexpr int P = decltype(par)::value;
-    constexpr int NH = (NV - P + 1) / 2;  // values P, P + 2, ...
+    constexpr int NH = (NV - P + kSplitWaves - 1) / kSplitWaves;  // values P, P + kSplitWaves, ...
     if constexpr (NH > 0) {
       Fp xs[NH][NT];
       x_for<NH>([&](auto h) {
-        x_for<NT>([&](auto t) { ld_fp_a8(xs[h][t], x_at(T, x_term_off(w, (P + 2 * h) * (1 + NT) + 1 + t))); });
+        x_for<NT>([&](auto t) {
+          ld_fp_a8(xs[h][t], x_at(T, x_term_off(w, (P + kSplitWaves * h) * (1 + NT) + 1 + t)));
+        });
       });
       __builtin_amdgcn_sched_barrier(0);
       uint32_t val[NH][10];
-      x_for<NH>([&](auto h) { x_lincomb_sum<W, NT, KP>(w, (P + 2 * h) * (1 + NT) + 1, xs[h], val[h]); });
+      x_for<NH>([&](auto h) { x_lincomb_sum<W, NT, KP>(w, (P + kSplitWaves * h) * (1 + NT) + 1, xs[h], val[h]); });
       x_for<NH>([&](auto h) {
-        const uint32_t dst = x_off(w, (P + 2 * h) * (1 + NT));
+        const uint32_t dst = x_off(w, (P + kSplitWaves * h) * (1 + NT));
         if (dst != 0xffffu) st_fp_a8(x_at(T, dst), val[h]);
       });
     }
   };
-  if (T.wave == 0) half(std::integral_constant<int, 0>{});
-  else half(std::integral_constant<int, 1>{});
+  if constexpr (kSplitWaves == 2) {
+    if (T.wave == 0) part(std::integral_constant<int, 0>{});
+    else part(std::integral_constant<int, 1>{});
+  } else {
+    x_for<kSplitWaves>([&](auto r) {
+      if (T.wave == decltype(r)::value) part(r);
+    });
+  }
 }
 
 // One round. Table layout per lane (16-bit entries): NV x (dst, NT x term),
@@ -428,7 +464,7 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     // the values are pinned before the first store, so the compiler cannot
     // sink a combination into its store's branch: the loads of all
     // combinations issue together instead of one LDS latency per combination
-    if (kTeamSplit && T.split) {  // a split team: wave w evaluates the values v = w mod 2
+    if (kTeamSplit && T.split) {  // a split team: the waves take turns over the values
       x_prepass_split<NV, NT, W, KP>(T, w);
       team_sync(T);
     } else {

@@ -176,7 +176,7 @@ def test_gt_and_g2_paths_agree():
             ("gt16c5", {"HG_GT_LEVEL": "2", "HG_GT_CHUNK": "5"}),
             # the signature pairing on 12-lane teams (bn256_sig12.hip) on the
             # padded context path too, and the 16-lane kernel everywhere (the
-            # 1024-check batch: two-wave teams, k_verify_sig_w2, unless
+            # 1024-check batch: two-wave teams, k_verify_sig_split<2>, unless
             # HG_SIG_W2=0)
             ("gt16sig12", {"HG_GT_LEVEL": "2", "HG_SIG12": "1"}),
             ("gt16sig16", {"HG_GT_LEVEL": "2", "HG_SIG12": "0"}),

@@ -161,7 +161,7 @@ def test_headline_lanes_match_oracle_committee(request, flavor):
 def test_pairing_kernels_give_identical_fe_values(engine, engine_cf):
     """hg_sig_pairing_device: the 16-lane k_verify_sig (padded, unpadded) and
     the 12-lane k_verify_sig12 (padded, unpadded, with k_sig_scalars /
-    k_sig_lines) and the two-wave k_verify_sig_w2 write byte-identical FE(Miller(G2Base at -sig)) values for
+    k_sig_lines) and the two-wave k_verify_sig_split<2> write byte-identical FE(Miller(G2Base at -sig)) values for
     valid signatures and the point at infinity, ragged n (teams of the last
     wave partly empty), both flavors. The verdict tests pin those values to
     the oracle through the comparison with the fold."""

@@ -39,7 +39,7 @@ HOT = {
     "k_verify_sig12ILb0E": (18800, "two_per_simd"),   # the headline's unpadded 12-lane kernel
     "k_verify_sig12ILb1E": (18800, "padded"),
     "k_verify_sigILi4ELb1ELb1E": (18880, "padded"),   # k_verify_sig<4, true, true>: sequential / latency
-    "k_verify_sig_w2": (30144, "padded"),             # the two-wave latency form
+    "k_verify_sig_splitILi2E": (30144, "padded"),     # the two-wave latency form
     "k_gt_chunks": (12000, None),
     "k_gt_combine": (9600, None),
 }

@@ -32,13 +32,13 @@ def main():
     bench.batch_latency(eng, head, dev, sizes=(32, 128), reps=5)  # warm
     out["batch_latency"] = bench.batch_latency(eng, head, dev, sizes=(1, 32, 128, 512, 2048, 4096), reps=25)
     # the pairing kernels alone (HIP events on one stream): the one-wave
-    # k_verify_sig and the two-wave k_verify_sig_w2, by batch size
+    # k_verify_sig and the two-wave k_verify_sig_split<2>, by batch size
     out["kernel_ms"] = {}
     ks = torch.cuda.Stream(dev)  # the events and the launches on one stream
     for n in (128, 1024, 2048):
         fe = torch.empty(n * 480, dtype=torch.uint8, device=dev)
         row = {}
-        for k, name in ((Engine.SIG_K16_PAD, "k_verify_sig"), (Engine.SIG_W2, "k_verify_sig_w2")):
+        for k, name in ((Engine.SIG_K16_PAD, "k_verify_sig"), (Engine.SIG_W2, "k_verify_sig_split<2>")):
             for _ in range(2):
                 eng.sig_pairing_device(head.d_sigs.data_ptr(), n, fe.data_ptr(), k, ks.cuda_stream)
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
