@@ -57,6 +57,7 @@ _SZ = ctypes.c_size_t
 _I = ctypes.c_int
 SIGNATURES = {
     "hg_version": (_I, []),
+    "hg_context_simds": (_I, [_P]),
     "hg_context_flavor": (_I, [_P]),
     "hg_create": (_I, [_I, _I, ctypes.POINTER(_P)]),
     "hg_destroy": (None, [_P]),
@@ -118,6 +119,7 @@ SIGNATURES = {
     "hg_lane_codes": (ctypes.POINTER(ctypes.c_int32), [_P]),
     "hg_lane_submit_device": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P]),
     "hg_lane_set_pairing_padding": (_I, [_P, _I]),
+    "hg_lane_set_latency_form": (_I, [_P, _I]),
     "hg_lane_stream": (_P, [_P]),
     "hg_service_config_init": (None, [_P]),
     "hg_service_create": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_P)]),

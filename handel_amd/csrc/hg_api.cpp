@@ -301,6 +301,7 @@ struct hg_lane {
   bool recorded = false;  // `done` marks the lane's last batch
   bool overlap = true;    // the fold beside the pairing kernel (on ws.side)
   bool pad = true;        // one pairing wave per SIMD (hg_lane_set_pairing_padding)
+  int w2_max = sig_w2_lane_max();  // the two-wave latency form up to this batch (hg_lane_set_latency_form)
   hipEvent_t ev_in = nullptr;  // hg_lane_submit_device: the caller's stream point
   size_t max_batch = 0, max_words = 0;
   uint8_t* h_in = nullptr;     // pinned staging
@@ -919,7 +920,7 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
         // batch at a time); lanes keep batches in flight, where twice the
         // waves per check costs throughput (HG_SIG_W2_LANE_MAX: A/B)
         launch_sig_pairing(d_sigs, c->flavor, (int)n, c->d_lines, ws.gt_fe.p, s, lane ? lane->pad : true,
-                           lane ? sig_w2_lane_max() : kSigW2MaxN);
+                           lane ? lane->w2_max : kSigW2MaxN);
       t.stop();
       HG_CHECK(c, hipStreamWaitEvent(ws.side, ws.ev_fork, 0));
       launch_agg_prologue(d_reqs, (int)n, (uint32_t)c->nreg, d_sigs, c->flavor, ws.pts1.p, d_codes, (int*)gw.hdr,
@@ -1068,6 +1069,13 @@ int hg_version(void) { return 2; }
 const char* hg_code_string(int code, int flavor) { return code_text(code, flavor); }
 
 const char* hg_processing_error_string(int code, int flavor) { return processing_text(code, flavor); }
+
+int hg_context_simds(hg_ctx* c) {
+  if (!c) return 0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return 0;
+  return 4 * cus;  // CDNA: four SIMDs per compute unit
+}
 
 int hg_context_flavor(hg_ctx* c) { return c ? c->flavor : -1; }
 
@@ -1894,6 +1902,13 @@ int hg_lane_set_pairing_padding(hg_lane* l, int pad) {
     HG_CHECK(c, l->ws.sig_lines.ensure(sig12_lines_bytes((int)l->max_batch)));
   }
   l->pad = pad != 0;
+  return HG_OK;
+}
+
+int hg_lane_set_latency_form(hg_lane* l, int max_checks) {
+  if (!l || max_checks < 0) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(l->c->mu);
+  l->w2_max = max_checks < kSigW2MaxN ? max_checks : kSigW2MaxN;
   return HG_OK;
 }
 

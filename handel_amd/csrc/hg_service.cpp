@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -51,6 +52,10 @@ struct Exec {
   // top table level now; returns HG_OK / HG_ERR_HASH_EOF or an error
   virtual int use_message(const uint8_t* m, size_t len, bool prepare) = 0;
   virtual int build_level(int level) = 0;  // every lane idle
+  // pairing waves the device holds at one per SIMD, and the lane's latency
+  // form for its next batch (hg_lane_set_latency_form)
+  virtual int simds() const { return 1024; }
+  virtual void latency_form(int, int) {}
 };
 
 struct GpuExec : Exec {
@@ -94,6 +99,9 @@ struct GpuExec : Exec {
     return rc;
   }
   int build_level(int level) override { return hg_prepare_aggregate_level(ctx, level); }
+  int simd_count = 0;
+  int simds() const override { return simd_count; }
+  void latency_form(int i, int max_checks) override { (void)hg_lane_set_latency_form(ln[i], max_checks); }
 };
 
 // CPU stand-in (hg_service_create_echo): codes from the request bytes
@@ -180,6 +188,7 @@ struct hg_service {
   struct LaneState {
     bool busy = false;
     std::vector<Pending> slots;
+    int waves = 0;  // pairing waves of the batch in flight
   };
   std::vector<LaneState> lanes;
   int busy = 0;
@@ -202,6 +211,8 @@ struct hg_service {
   // adopted[ch] once the dispatcher has swept the ring the handle left
   std::vector<uint8_t> adopted;
   uint32_t seen_orphans = 0;
+  bool w2_policy = true;  // HG_SERVICE_W2=0: the one-wave kernel only
+  static constexpr int kW2MaxChecks = 2048;  // the latency form's largest batch (bn256_gt.h kSigW2MaxN)
 
   bool intake();
   void complete(int lane, const int32_t* codes, int32_t fail);
@@ -423,6 +434,16 @@ void hg_service::launch(int lane) {
       memcpy(w + wo, s->words(), 8ull * nw);
       wo += nw;
     }
+    // the two-wave latency form while the batches in flight leave a SIMD
+    // for each of its waves (padded kernels: one wave per SIMD), else the
+    // one-wave kernel; HG_SERVICE_W2=0 never
+    const int n = (int)take.size(), one = (n + 3) / 4;
+    int used = 0;
+    for (const LaneState& o : lanes)
+      if (o.busy) used += o.waves;
+    const bool w2 = w2_policy && n <= kW2MaxChecks && used + 2 * one <= ex->simds();
+    ex->latency_form(lane, w2 ? kW2MaxChecks : 0);
+    lanes[lane].waves = w2 ? 2 * one : one;
     rc = ex->submit(lane);
   }
   LaneState& L = lanes[lane];
@@ -595,6 +616,8 @@ int hg_service_create(hg_ctx* ctx, const char* name, const hg_service_config* cf
     delete s;
     return rc;
   }
+  g->simd_count = hg_context_simds(ctx);
+  if (const char* e = getenv("HG_SERVICE_W2")) s->w2_policy = atoi(e) != 0;
   s->ex = g;
   g->warm_up();  // under the context's current message, if it has one
   start(s);

@@ -444,6 +444,11 @@ class DeviceLane:
         if not pad:
             engine._check(self.L.hg_lane_set_pairing_padding(self.h, 0), "hg_lane_set_pairing_padding")
 
+    def set_latency_form(self, max_checks: int):
+        """hg_lane_set_latency_form: padded batches of at most max_checks
+        checks run the two-wave pairing kernel (0: never)."""
+        self.engine._check(self.L.hg_lane_set_latency_form(self.h, int(max_checks)), "hg_lane_set_latency_form")
+
     def close(self):
         if getattr(self, "h", None):
             self.L.hg_lane_destroy(self.h)

@@ -98,6 +98,9 @@ const char* hg_processing_error_string(int code, int flavor);
 int hg_version(void);
 /* The context's flavor (HG_FLAVOR_GO / HG_FLAVOR_CF), -1 for NULL. */
 int hg_context_flavor(hg_ctx* ctx);
+/* SIMDs of the context's device (compute units x 4): the pairing waves it
+ * holds at one wave per SIMD (the padded kernels); 0 on error. */
+int hg_context_simds(hg_ctx* ctx);
 
 /* Registry.Identities(...).PublicKey() source: uploads n marshalled G2
  * public keys (PublicKey.UnmarshalBinary, bn256/go/bn256.go:113-120), decoding
@@ -400,6 +403,13 @@ int hg_lane_submit_device(hg_lane* lane, const hg_request* d_reqs, size_t n, con
  * lowest latency for one batch); 0: unpadded, so two batches in flight put
  * two pairing waves on a SIMD (throughput of a continuous stream). */
 int hg_lane_set_pairing_padding(hg_lane* lane, int pad);
+/* The latency form on a padded lane: its batches of at most max_checks
+ * (<= 2048) checks run the pairing with each check's team over two waves
+ * (k_verify_sig_split<2>: ~9 % shorter, twice the waves); 0 (the default,
+ * or HG_SIG_W2_LANE_MAX): never. The verifier service sets it per batch while
+ * the batches in flight leave a SIMD per wave. Takes effect at the next
+ * submission. */
+int hg_lane_set_latency_form(hg_lane* lane, int max_checks);
 /* The lane's launch stream (a hipStream_t): passed as hg_lane_submit_device's
  * `stream`, the lane orders its batches only after its own earlier ones. */
 void* hg_lane_stream(hg_lane* lane);

@@ -39,6 +39,7 @@
 extern "C" {
 size_t hg_registry_size(hg_ctx*) { return 0; }
 int hg_context_flavor(hg_ctx*) { return 0; }
+int hg_context_simds(hg_ctx*) { return 0; }
 int hg_set_message(hg_ctx*, const uint8_t*, size_t) { return HG_ERR_DEVICE; }
 int hg_prepare_aggregate_msg(hg_ctx*, const uint8_t*, size_t) { return HG_ERR_DEVICE; }
 int hg_prepare_aggregate_level(hg_ctx*, int) { return HG_ERR_DEVICE; }
@@ -49,6 +50,7 @@ int hg_lane_submit(hg_lane*) { return HG_ERR_DEVICE; }
 int hg_lane_query(hg_lane*) { return -1; }
 int hg_lane_wait(hg_lane*) { return HG_ERR_DEVICE; }
 const int32_t* hg_lane_codes(hg_lane*) { return nullptr; }
+int hg_lane_set_latency_form(hg_lane*, int) { return HG_ERR_DEVICE; }
 }
 
 using namespace hgshm;

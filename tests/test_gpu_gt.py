@@ -490,12 +490,14 @@ def test_fused_bitset_matches_pack(level, overlap):
         e.close()
 
 
-@pytest.mark.parametrize("pad", [False, True], ids=["unpadded", "padded"])
+@pytest.mark.parametrize("pad", [False, True, "latency"], ids=["unpadded", "padded", "latency"])
 def test_device_lanes_keep_batches_in_flight(pad):
     """hg_lane_submit_device (bench.py's headline): two lanes of one context
     alternate on a batch resident in HBM, each on its own torch stream, two
     batches in flight; every round's codes are the expected verdicts (the
-    oracle's: test_gt_and_g2_paths_agree) and its bitset packs them."""
+    oracle's: test_gt_and_g2_paths_agree) and its bitset packs them.
+    'latency': padded lanes in the two-wave latency form
+    (hg_lane_set_latency_form, as the verifier service sets it)."""
     import torch
 
     import bench
@@ -512,7 +514,10 @@ def test_device_lanes_keep_batches_in_flight(pad):
         n = len(reqs)
         d_reqs, d_words = bench._dev_bytes(reqs.tobytes(), dev), bench._dev_bytes(words.tobytes(), dev)
         d_sigs = bench._dev_bytes(bytes(sigs), dev)
-        lanes = [DeviceLane(e, n, pad=pad) for _ in range(2)]
+        lanes = [DeviceLane(e, n, pad=pad is not False) for _ in range(2)]
+        if pad == "latency":
+            for ln in lanes:
+                ln.set_latency_form(2048)
         streams = [torch.cuda.Stream(dev) for _ in lanes]
         codes = [torch.full((n,), -1, dtype=torch.int32, device=dev) for _ in lanes]
         bits = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev) for _ in lanes]
