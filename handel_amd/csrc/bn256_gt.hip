@@ -54,6 +54,9 @@ HG_DEV void fold_regs_init(const Team& T) {
   team_sync();
 }
 using IMulF = XInst<XP_MUL12F, S_A, S_A, S_B>;  // A = A * B in the FOLD region
+// (the hint re-fetches the same round's words: measured 1-2 % faster for the
+// fold than keeping them, which frees 10 VGPRs but not a wave per SIMD,
+// profiles/r05fb_fold_refetch_ab.json)
 HG_DEV void fold_mul(const Team& T, XStream& S) {
   team_sync();
   IMulF::run(T, S, xh<IMulF>());
@@ -389,7 +392,13 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_gt_plan(const AggRequest* r
 // The next term is fetched from HBM into registers while the current product
 // runs.
 static_assert(kGtChunkTeams == kTeams12, "k_gt_chunks' teams per workgroup");
-__global__ __launch_bounds__(64) void k_gt_chunks(const Gt* win, const Gt* blk, const uint32_t* terms,
+// minimum waves per SIMD the compiler sizes k_gt_chunks' registers for (A/B
+// builds: 3 -> 168 VGPRs with 37 spills, fold alone 0.59 -> 0.66 ms,
+// profiles/r05fa_fold_occupancy_ab.json; 1 = the compiler's choice, 200 VGPRs)
+#ifndef HG_CHUNK_WAVES
+#define HG_CHUNK_WAVES 1
+#endif
+__global__ __launch_bounds__(64, HG_CHUNK_WAVES) void k_gt_chunks(const Gt* win, const Gt* blk, const uint32_t* terms,
                                                   const int2* ord, int cap, const GtReq* plan, const GtHdr* hdr,
                                                   int chunk, Gt* partial, Gt* y) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams12 * kFoldWords];
