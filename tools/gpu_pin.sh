@@ -22,6 +22,6 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run -- pyth
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $OUT/fetch -o run -- python3 $H > $OUT/fetch.log 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $OUT/write -o run -- python3 $H > $OUT/write.log 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY --kernel-include-regex "$K" -d $OUT/sq -o run -- python3 $H > $OUT/sq.log 2>&1 &&
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_verify\(" -d $OUT/single_fetch -o run -- python3 $S > $OUT/single_fetch.log 2>&1 &&
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_verify\(" -d $OUT/single_write -o run -- python3 $S > $OUT/single_write.log 2>&1 &&
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_verify<" -d $OUT/single_fetch -o run -- python3 $S > $OUT/single_fetch.log 2>&1 &&
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_verify<" -d $OUT/single_write -o run -- python3 $S > $OUT/single_write.log 2>&1 &&
 python3 tools/rocpd_summary.py $OUT $OUT/${R}_driver && rm -f $OUT/*/*.db
