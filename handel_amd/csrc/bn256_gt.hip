@@ -229,7 +229,10 @@ HG_DEV const Gt* term_ptr(uint32_t t, const Gt* win, const Gt* blk) {
 // then the window-table index of every nonzero byte of the folded mask in
 // registry-aligned windows, and the owner of each chunk. An empty bitset is
 // the reference's nil-aggregate panic (HG_ERR_EMPTY_AGG).
-static constexpr int kPlanWaves = 16;  // requests per k_gt_plan workgroup (one wave each)
+#ifndef HG_PLAN_WAVES  // A/B knob: 4 measured slower (profiles/r05sk_small_kernels_ab.json)
+#define HG_PLAN_WAVES 16
+#endif
+static constexpr int kPlanWaves = HG_PLAN_WAVES;  // requests per k_gt_plan workgroup (one wave each)
 template <int W>
 HG_DEV uint32_t nz_units(uint64_t x) {
   return W == 8 ? nz_bytes(x) : nz_halves(x);

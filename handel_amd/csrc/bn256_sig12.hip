@@ -41,13 +41,20 @@
 
 namespace hg {
 
+// threads per workgroup of the two small kernels ahead of the pairing (A/B
+// knob: 64 measured slower, profiles/r05sk_small_kernels_ab.json)
+#ifndef HG_SIG_LINE_BLOCK
+#define HG_SIG_LINE_BLOCK 256
+#endif
+static constexpr int kLineBlock = HG_SIG_LINE_BLOCK;
+
 // the signature's evaluation scalars: sc[2c] = x_sig, sc[2c + 1] = -y_sig
 // (both 0 at infinity: e(inf, G2Base) = 1, every line evaluates to w^3, which
 // the final exponentiation maps to 1 — bn256_gt.hip team_miller_sig). A
 // signature that fails to decode gives meaningless lines: its FE value is
 // never compared (its code is the decode error, k_agg_prologue).
-__global__ __launch_bounds__(256) void k_sig_scalars(const uint8_t* sig_bytes, int flavor, int n, Fp* sc) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(kLineBlock) void k_sig_scalars(const uint8_t* sig_bytes, int flavor, int n, Fp* sc) {
+  const int c = blockIdx.x * kLineBlock + threadIdx.x;
   if (c >= n) return;
   PointG1 sg;
   (void)decode_g1_one(sig_bytes + (size_t)c * 64, flavor, sg);
@@ -62,8 +69,8 @@ __global__ __launch_bounds__(256) void k_sig_scalars(const uint8_t* sig_bytes, i
 // ev[(s * n + c) * 4 + j] = component j of line s at -sig_c: one Montgomery
 // product per thread (FB = bx * x_sig, FC = cy * -y_sig); grid (4n / 256,
 // lines), consecutive threads on consecutive 40-byte results
-__global__ __launch_bounds__(256) void k_sig_lines(const Fp* sc, int n, const LineCoef* tab, Fp* ev) {
-  const int t = blockIdx.x * 256 + threadIdx.x;  // 4 c + j
+__global__ __launch_bounds__(kLineBlock) void k_sig_lines(const Fp* sc, int n, const LineCoef* tab, Fp* ev) {
+  const int t = blockIdx.x * kLineBlock + threadIdx.x;  // 4 c + j
   if (t >= 4 * n) return;
   const int s = blockIdx.y;
   const int j = t & 3;
@@ -204,8 +211,8 @@ void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef
   if (n <= 0) return;
   Gt* park = (Gt*)((uint8_t*)ev + sig12_park_offset(n));
   Fp* sc = (Fp*)((uint8_t*)ev + sig12_scalar_offset(n));
-  k_sig_scalars<<<(n + 255) / 256, 256, 0, s>>>(sigs, flavor, n, sc);
-  k_sig_lines<<<dim3((4 * n + 255) / 256, kNumLines), 256, 0, s>>>(sc, n, tab, ev);
+  k_sig_scalars<<<(n + kLineBlock - 1) / kLineBlock, kLineBlock, 0, s>>>(sigs, flavor, n, sc);
+  k_sig_lines<<<dim3((4 * n + kLineBlock - 1) / kLineBlock, kNumLines), kLineBlock, 0, s>>>(sc, n, tab, ev);
   const int blocks = (n + kTeams12 - 1) / kTeams12;
   if (pad) k_verify_sig12<true><<<blocks, 64, 0, s>>>(ev, n, fe, park);
   else k_verify_sig12<false><<<blocks, 64, 0, s>>>(ev, n, fe, park);
