@@ -64,3 +64,13 @@ def test_exact_error_strings_without_gpu():
     assert proc(_lib.HG_ERR_HASH_EOF) == "handel: EOF"
     assert proc(_lib.HG_ERR_LEVEL) == "handel: inconsistent bitset with given level"
     assert "handel: handel:" not in "".join(proc(c) for c in range(14))
+
+
+def test_null_handles_are_refused_without_gpu():
+    """Entry points that take a context or lane refuse NULL before touching
+    the device (no GPU here: nothing else may run)."""
+    L = _lib.load(build_if_missing=False)
+    assert L.hg_context_simds(None) == 0
+    assert L.hg_lane_set_latency_form(None, 2048) == _lib.HG_ERR_ARG
+    assert L.hg_lane_set_pairing_padding(None, 1) == _lib.HG_ERR_ARG
+    assert L.hg_sig_pairing_device(None, None, 0, None, 0, None) == _lib.HG_ERR_ARG
