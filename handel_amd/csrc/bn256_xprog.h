@@ -404,6 +404,17 @@ HG_DEV void x_job_split(const Team& T, const uint32_t (&w)[W], int base, Fp a0, 
   __syncthreads();  // the round's end
 }
 
+// Split teams' pre-pass: 1 = the waves share the values (a workgroup barrier
+// before the products); 0 = every wave evaluates every value and stores it
+// (the waves store identical words), so each wave reads back its own stores
+// and a wave-level sync suffices. 0 measured slower: 0.768 vs 0.745 ms for 128
+// checks (profiles/r05lv_split_prepass_ab.json) — the barrier is cheaper than
+// the lincombs it saves on wave 0's path
+#ifndef HG_SPLIT_PREPASS
+#define HG_SPLIT_PREPASS 1
+#endif
+static constexpr bool kSplitPrepass = HG_SPLIT_PREPASS != 0;
+
 // the pre-pass of a split team's round: wave r evaluates the values v = r,
 // r + kSplitWaves, ...
 template <int NV, int NT, int W, int KP>
@@ -464,7 +475,7 @@ HG_DEV void x_round(const Team& T, XStream& S, int off, XHint nxt) {
     // the values are pinned before the first store, so the compiler cannot
     // sink a combination into its store's branch: the loads of all
     // combinations issue together instead of one LDS latency per combination
-    if (kTeamSplit && T.split) {  // a split team: the waves take turns over the values
+    if (kTeamSplit && kSplitPrepass && T.split) {  // a split team: the waves take turns over the values
       x_prepass_split<NV, NT, W, KP>(T, w);
       team_sync(T);
     } else {
