@@ -1175,6 +1175,8 @@ def main():
         extra["batch_latency"] = {
             "what": "one batch submitted alone and waited for (median of 15), first n headline requests: the "
                     "per-check latency floor a one-check-at-a-time evaluator (processing.go:228-287) sees",
+            "pairing_kernel": "k_verify_sig_split<2> (two waves per check, DESIGN.md 3e) for n <= 2048, "
+                              "k_verify_sig<4, true> above",
             **batch_latency(eng, head, dev)}
         progress("handel_run_volume")
         extra["handel_run_volume"] = handel_run_volume(dev, stream, local_dev)
