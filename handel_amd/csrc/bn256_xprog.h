@@ -397,9 +397,14 @@ HG_DEV void x_job_split(const Team& T, const uint32_t (&w)[W], int base, Fp a0, 
     }
   });
   Fp r;
+#ifdef HG_SPLIT_NOREDC  // timing probe only (wrong values): the reduction's share of the critical path
+#pragma unroll
+  for (int l = 0; l < 10; l++) r.l[l] = (uint32_t)acc.c[11 + l] & kMask;
+#else
   if constexpr (NL > 0 && LZ) acc_reduce_wide_lazy<0>(r, acc);
   else if constexpr (NL > 0) acc_reduce_wide<0>(r, acc);
   else acc_reduce<0>(r, acc);
+#endif
   if (dst != 0xffffu) st_fp_a8(x_at(T, dst), r.l);
   __syncthreads();  // the round's end
 }
