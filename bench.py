@@ -282,6 +282,26 @@ def rocprof_kernel_us(pattern: str):
     return None, None
 
 
+def rocprof_busy_ms(inflight: int):
+    """Per-step device-busy ms of the headline (the union of every kernel
+    interval inside the timed region / steps) from the newest committed
+    summary of a kernel trace of the driver's invocation with the same batches
+    in flight (profiles/*_driver_busy.json, tools/busy_summary.py); (None,
+    None) if there is none."""
+    import glob
+    import re
+
+    def key(path):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_driver_busy.json")), key=key, reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("batches_in_flight") == inflight and d.get("busy_ms_per_step"):
+            return float(d["busy_ms_per_step"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def _cgroup_quota_cpus():
     """CPUs of CPU time the cgroup grants this process (cgroup v2 cpu.max
     "quota period"), None when unlimited or unreadable."""
@@ -401,6 +421,58 @@ def cpu_baseline_aggregate(reg: bytes, reqs, words, sigs: bytes, expect: np.ndar
     return out
 
 
+def clock_marks() -> dict:
+    """Now, in ns, on every host clock a profiler's timestamps may be taken on."""
+    return {"monotonic": time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+            "boottime": time.clock_gettime_ns(time.CLOCK_BOOTTIME),
+            "realtime": time.clock_gettime_ns(time.CLOCK_REALTIME)}
+
+
+def cpu_baseline_on_rank0(rank: int, dist: bool, args, run):
+    """The CPU baseline beside every world size (north_star: the CPU figure
+    next to the GPU's, in the same run): rank 0 runs run() after the timed
+    regions while the other ranks wait at a barrier, so it never overlaps a
+    timed step and every rank leaves together. None when --no-cpu."""
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        try:
+            cpu = run()
+        except Exception as e:  # pragma: no cover - reported, not fatal
+            cpu = {"error": str(e)}
+    if dist:
+        import torch.distributed as tdist
+
+        tdist.barrier()
+    return cpu
+
+
+def cpu_probe_workload(n_reg: int = 8, n: int = 4):
+    """A tiny config-3-shaped workload made with the CPU oracle (the
+    --cpu-probe test hook: no GPU): a registry of n_reg seeded keys, n
+    multisignatures over the whole registry, every 2nd tampered."""
+    from oracle import ref_lib as R
+
+    rng = np.random.default_rng(5)
+    kb = seeded_scalars(n_reg, 5)
+    ks = [int.from_bytes(kb[32 * i:32 * i + 32], "big") for i in range(n_reg)]
+    reg = R.g2_scalar_base(kb)
+    reqs, words, sigs, expect = [], [], b"", []
+    for i in range(n):
+        bits = rng.random(n_reg) < 0.7
+        bits[i % n_reg] = True
+        sk = sum(k for k, b in zip(ks, bits) if b) % ORDER
+        sig = R.sign(LIB_MESSAGE, sk.to_bytes(32, "big"))
+        if i % 2:
+            sig = R.g1_add(sig, G1_GEN_BYTES)
+        reqs.append((0, n_reg, n_reg, len(words)))
+        words.append(int(sum(1 << j for j in range(n_reg) if bits[j])))
+        sigs += sig
+        expect.append(i % 2)
+    from handel_amd.engine import REQ_DTYPE as RD
+
+    return reg, np.array(reqs, dtype=RD), np.array(words, dtype=np.uint64), sigs, np.array(expect, dtype=np.int32)
+
+
 class Timer:
     """Barrier + synchronize on both sides of the timed region, max over ranks
     (every rank's own time is kept in `rank_times`)."""
@@ -408,6 +480,7 @@ class Timer:
     def __init__(self, dev, dist, coll_dev, world: int = 1):
         self.dev, self.dist, self.coll_dev, self.world = dev, dist, coll_dev, world
         self.rank_times = []
+        self.marks = {}
 
     def _sync(self):
         if self.dev.type == "cuda":  # (a CPU device: the gloo test of this class)
@@ -450,10 +523,15 @@ class Timer:
             import torch.distributed as tdist
             tdist.barrier()
         self._sync()
+        m0 = clock_marks()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         self._sync()
+        m1 = clock_marks()
+        # the timed region on the host clocks a kernel trace may use
+        # (tools/busy_summary.py finds the step kernels inside it)
+        self.marks = {k: [m0[k], m1[k]] for k in m0}
         if self.dist:
             tdist.barrier()
         dt = time.perf_counter() - t0
@@ -669,26 +747,49 @@ def batch_latency(eng: Engine, head, dev, sizes=(32, 128, 512, 4096), reps: int 
     return out
 
 
-def config4_proxy(model: str, timeout: int = 180):
+def under_profiler() -> bool:
+    """A rocprofv3 run: its tool library is preloaded into this process and
+    every process started from it."""
+    return "rocprofiler" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def config4_proxy(model: str, timeout: int = 180, extra=()):
     """Config 4's verification load in simul's single-host process layout
     (tests/native/handel_proxy.c): 8 processes x 250 Handel instances x 45
     checks on a 2000-key registry, one check in flight per instance, every
     verdict checked against the expected one. model 'service': one GPU-owning
     verifier process (hg_service_*, 8 lanes) and 8 client processes that load
     only libhandel_client.so; 'contexts': every process its own context, GT
-    tables and batcher (the r03 layout). Not Handel completion time."""
+    tables and batcher (the r03 layout). Not Handel completion time.
+
+    The proxy runs in a session of its own: on a timeout the whole process
+    group (the proxy and the processes it forked) is killed, and the line
+    keeps the tail of what they printed (each process reports its phases on
+    stderr), so a stall names the phase it stalled in."""
+    import signal
     import subprocess
 
     from handel_amd import build as B
 
     args = ["-D", "1", "-P", "1", "-l", "8"] if model == "service" else ["-D", "0", "-P", "1"]
     try:
-        r = subprocess.run([B.HANDEL_PROXY, B.LIB, *args], capture_output=True, text=True, timeout=timeout)
-    except (OSError, subprocess.TimeoutExpired) as e:  # pragma: no cover - reported, not fatal
+        pr = subprocess.Popen([B.HANDEL_PROXY, B.LIB, *args, *extra], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, start_new_session=True)
+    except OSError as e:  # pragma: no cover - reported, not fatal
         return {"error": str(e)}
-    if r.returncode != 0:
-        return {"error": f"rc {r.returncode}: {r.stderr[-500:]}"}
-    d = json.loads(r.stdout.strip().splitlines()[-1])
+    try:
+        out, err = pr.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(pr.pid, signal.SIGKILL)  # the group this call started (its own session)
+        except ProcessLookupError:  # pragma: no cover
+            pass
+        out, err = pr.communicate()
+        return {"error": f"timed out after {timeout} s (process group killed)", "under_profiler": under_profiler(),
+                "stderr_tail": err[-2500:], "stdout_tail": out[-500:]}
+    if pr.returncode != 0:
+        return {"error": f"rc {pr.returncode}", "stderr_tail": err[-2500:]}
+    d = json.loads(out.strip().splitlines()[-1])
     keep = ("model", "procs", "instances_per_proc", "registry", "checks_per_instance", "lanes", "hw_queues",
             "requests", "batches", "mean_batch", "wall_ms", "throughput", "latency_us", "hbm_total_bytes",
             "contexts", "mismatches")
@@ -810,6 +911,9 @@ def main():
     ap.add_argument("--launch-probe", action="store_true",
                     help="test hook: start the ranks, join the process group (gloo, no device), print the "
                          "world each rank saw, exit")
+    ap.add_argument("--cpu-probe", action="store_true",
+                    help="test hook: start the ranks (gloo, no device), run the CPU baseline's rank-0 leg on a tiny "
+                         "oracle-made workload exactly as the bench does after its timed regions, print rank 0's line")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=4096)
@@ -832,6 +936,19 @@ def main():
         # the driver's `python bench.py --gpus N`: one rank per GPU, started here
         raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = world_from_env(args.gpus)
+    if args.cpu_probe:
+        import torch.distributed as tdist
+
+        if world > 1:
+            tdist.init_process_group("gloo")
+        reg, reqs, words, sigs, expect = cpu_probe_workload()
+        cpu = cpu_baseline_on_rank0(rank, world > 1, args, lambda: cpu_baseline_aggregate(
+            reg, reqs, words, sigs, expect, len(reqs), min_wall=0.2))
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "cpu_baseline": cpu}))
+        if world > 1:
+            tdist.destroy_process_group()
+        return
     if args.launch_probe:
         import torch.distributed as tdist
 
@@ -862,7 +979,10 @@ def main():
     if want_q and (os.environ.get("HG_BENCH_HW_QUEUES") or int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) < want_q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
-    dist = world > 1
+    # HG_BENCH_FORCE_PG=1 (a test hook: tests/test_gpu_rccl.py): the process
+    # group and every collective of the N-rank path even with one rank, so
+    # the RCCL branch runs on a one-GPU box exactly as each rank of N runs it
+    dist = world > 1 or os.environ.get("HG_BENCH_FORCE_PG") == "1"
     # HG_BENCH_BACKEND=gloo is a rehearsal mode for boxes with fewer GPUs than
     # ranks (ranks share devices round-robin, collectives on host copies); the
     # production path is one rank per GPU over RCCL ("nccl").
@@ -914,7 +1034,7 @@ def main():
                                               for _ in range(world)]
             # the gather runs on the lane's own stream (wrapped for torch), right
             # after the lane's verdicts; the lane's next batch follows it there
-            lane_out.append((torch.cuda.ExternalStream(lanes[-1].stream, device=dev) if world > 1 else None,
+            lane_out.append((torch.cuda.ExternalStream(lanes[-1].stream, device=dev) if dist else None,
                              codes_i, bits_i, gath_i))
     turn = [0]
 
@@ -922,7 +1042,7 @@ def main():
         i = turn[0] % inflight
         turn[0] += 1
         st, codes_i, bits_i, gath_i = lane_out[i]
-        if world == 1:
+        if not dist:
             # nothing reads the verdicts between steps (the gather is the
             # identity): the lane orders each batch after its own previous one
             lanes[i].submit_device(head.d_reqs.data_ptr(), n, head.d_words.data_ptr(), head.d_sigs.data_ptr(),
@@ -944,6 +1064,7 @@ def main():
     progress(f"headline: {inflight} in flight, prewarm / warmup / {args.steps} timed steps")
     prewarm_steps = timer.prewarm(step, args.prewarm)
     dt = timer.run(step, args.steps, args.warmup)
+    head_marks = dict(timer.marks)
     rank_ms = [round(t / args.steps * 1e3, 4) for t in timer.rank_times]
     # every rank's gathered bitsets: each rank tampers every 8th aggregate of
     # its own batch, so all world bitsets equal this rank's expected one
@@ -997,19 +1118,29 @@ def main():
                     f"product each) + {n} x {FPMUL_PER_SIG_PAIRING} Fp-mul (one pairing + final exponentiation "
                     f"per check), x {MADS_PER_FPMUL} u32 mads",
                     rocprof_pattern=sig_kernel + r"|k_gt_compare_bits")
+    # frac_rocprof: the same work over the device-busy time per step of a
+    # committed kernel trace of this invocation (the union of the timed
+    # region's kernel intervals / steps, tools/busy_summary.py); the older
+    # per-launch form stays as frac_rocprof_per_launch (with batches in
+    # flight a launch lasts longer than a step, so that form is low)
+    if "frac_rocprof" in roof:
+        roof["frac_rocprof_per_launch"] = roof.pop("frac_rocprof")
+        roof["rocprof_kernel_ms_per_launch"] = roof.pop("rocprof_kernel_ms")
+    busy_ms, busy_src = rocprof_busy_ms(inflight)
+    if busy_ms:
+        roof["frac_rocprof"] = round(impl_fpmul * MADS_PER_FPMUL / (busy_ms * 1e-3) / 1e12 / P_MAD_TOPS, 4)
+        roof["rocprof_busy_ms_per_step"] = busy_ms
+        roof["rocprof_busy_source"] = busy_src
+    roof["frac_rocprof_note"] = (
+        "the same implemented work over the device-busy time per timed step in a kernel trace of the driver's "
+        "invocation (every kernel interval inside the timed region merged, / steps; the trace's own line records "
+        "the region): reproduces `frac` from a committed profile. frac_rocprof_per_launch: over the rocprof average "
+        "launch duration of the step's pairing kernels and comparison" + (
+            f" — with {inflight} batches in flight two launches share the SIMDs, so a launch lasts longer than a "
+            "step and that fraction is below `frac`" if inflight > 1 else ""))
     if inflight > 1:
-        roof["frac_rocprof_note"] = (
-            "the same work over the rocprof average LAUNCH duration of the headline's pairing kernels (k_verify_sig12<false> "
-            "and its line kernels, which only the headline's unpadded lanes launch) plus the comparison, in the "
-            "driver-invocation profile: with "
-            f"{inflight} batches in flight two launches share the SIMDs, so a launch lasts longer than a step and "
-            "this per-launch fraction is below `frac`")
         roof["sequential_submit_ms"] = round(ph["submit"], 4)
         roof["sequential_frac"] = round(impl_fpmul * MADS_PER_FPMUL / (ph["submit"] * 1e-3) / 1e12 / P_MAD_TOPS, 4)
-    else:
-        roof["frac_rocprof_note"] = ("the same work over the rocprof averages of the step's critical path (the "
-                                     "pairing kernel, then the comparison; the fold runs beside it) in the "
-                                     "driver-invocation profile")
     roof["kernels_ms"] = {"fold": round(ph["fold"], 4), "k_verify": round(ph["verify"], 4),
                           "submit": round(ph["submit"], 4)}
     # the reference algorithm's work over the same time: a rate, not a
@@ -1077,11 +1208,10 @@ def main():
             "workload": f"config 2: {n} independent BLS pairing checks per GPU (lib.Message, 1/8 tampered)",
             "roofline": roofline(single.fpmul, sph["verify"], "k_verify", r"k_verify(?!_)",
                                  f"{FPMUL_PER_CHECK} Fp-mul x {MADS_PER_FPMUL} u32 mads per check")}
-        if rank == 0 and world == 1 and not args.no_cpu:
-            try:
-                extra["single"]["cpu_baseline"] = cpu_baseline_single(single.pks, single.sigs, single.expect)
-            except Exception as e:  # pragma: no cover - reported, not fatal
-                extra["single"]["cpu_baseline"] = {"error": str(e)}
+        # at every world size: rank 0 after this line's timed region, the
+        # other ranks at a barrier
+        extra["single"]["cpu_baseline"] = cpu_baseline_on_rank0(
+            rank, dist, args, lambda: cpu_baseline_single(single.pks, single.sigs, single.expect))
         del single
         # config 2 with registry keys (the p2p aggregator's verifyPacket,
         # simul/p2p/aggregator.go:244): one-key aggregate requests on the head
@@ -1189,13 +1319,11 @@ def main():
                         "one check in flight per instance) on this GPU; checks/s, per-check latency, HBM",
                 "service": config4_proxy("service"), "contexts": config4_proxy("contexts")}
 
-    cpu = None
-    progress("CPU baseline" if rank == 0 and world == 1 and not args.no_cpu else "done")
-    if rank == 0 and world == 1 and not args.no_cpu:
-        try:
-            cpu = cpu_baseline_aggregate(head.reg, head.reqs, head.words, head.sigs, head.expect, args.cpu_sample)
-        except Exception as e:  # pragma: no cover - reported, not fatal
-            cpu = {"error": str(e)}
+    progress("CPU baseline" if rank == 0 and not args.no_cpu else "done")
+    # at every world size (north_star: the CPU figure beside each N): rank 0,
+    # after every timed region, the other ranks waiting at a barrier
+    cpu = cpu_baseline_on_rank0(rank, dist, args, lambda: cpu_baseline_aggregate(
+        head.reg, head.reqs, head.words, head.sigs, head.expect, args.cpu_sample))
     if rank == 0:
         workload = (f"config 5: one committee of {n_reg} signers per GPU, {n} multisigs at random Handel levels"
                     if args.committees else
@@ -1211,6 +1339,7 @@ def main():
             "batches_in_flight": inflight,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
+            "timed_region_ns": head_marks,
             "prewarm": {"seconds": args.prewarm, "steps": prewarm_steps, "what": "untimed headline steps before the "
                         "warmup steps (GPU clocks settled whatever the warmup count)"},
             "gather": {**gather_check, "what": "every rank's all-gathered verdict bitset checked against the expected "

@@ -53,6 +53,7 @@ type Client struct {
 	hmu       sync.RWMutex
 	closed    bool
 	closeOnce sync.Once
+	texts     map[int32]string // code -> processing.go error text (read-only after Open)
 }
 
 var errClosed = errors.New("hipsvc: client closed")
@@ -66,7 +67,13 @@ func Open(name string) (*Client, error) {
 		return nil, fmt.Errorf("hipsvc: cannot attach to %s (code %d)", name, int(rc))
 	}
 	c := &Client{h: h, waiting: map[uint64]chan int32{}, early: map[uint64]int32{}, done: make(chan struct{}),
-		polled: make(chan struct{})}
+		polled: make(chan struct{}), texts: map[int32]string{}}
+	// every code's text, taken while the handle is certainly open: a verdict
+	// delivered as Close runs keeps its own error (handel_gpu.h hg_code values
+	// 0..29, 100, 101; anything else maps to "device error")
+	for code := int32(0); code <= 101; code++ {
+		c.texts[code] = C.GoString(C.hg_client_processing_error_string(h, C.int(code)))
+	}
 	go c.poll()
 	return c, nil
 }
@@ -190,18 +197,18 @@ func (c *Client) Verify(msg []byte, r Request) error {
 	return c.codeError(code)
 }
 
-// codeError maps an hg_code to processing.go's error (nil for HG_OK). The
-// texts need no handle beyond the flavor (hg_client_processing_error_string).
+// codeError maps an hg_code to processing.go's error (nil for HG_OK), from
+// the table Open took (hg_client_processing_error_string depends only on the
+// flavor), so it never needs the handle: a real verdict that arrives while
+// Close runs stays that verdict, not errClosed.
 func (c *Client) codeError(code int32) error {
 	if code == C.HG_OK {
 		return nil
 	}
-	c.hmu.RLock()
-	defer c.hmu.RUnlock()
-	if c.closed {
-		return errClosed
+	if t, ok := c.texts[code]; ok {
+		return errors.New(t)
 	}
-	return errors.New(C.GoString(C.hg_client_processing_error_string(c.h, C.int(code))))
+	return errors.New("device error")
 }
 
 // Verifier is a handel.BatchVerifier (go/handel/batched_processing.go) over

@@ -89,7 +89,10 @@ void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef
 // (the latency mode: one wave per SIMD, where its shorter per-wave program
 // and the absence of the line kernels give the lower batch latency).
 // HG_SIG12=1 / 0 forces one kernel for every launch (A/B).
-bool sig12_for(bool pad);
+// n: the batch's checks; above kSig12MaxN the 12-lane path (whose line kernel
+// indexes 4 n threads in int) is never taken
+constexpr int kSig12MaxN = 1 << 28;
+bool sig12_for(bool pad, size_t n = 0);
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s);
 // the same, and the verdict bitset (ceil(n / 8) bytes, hg_pack_verdicts_device's layout)
 void launch_gt_compare_bits(const Gt* fe, const Gt* y, int n, int32_t* codes, uint8_t* bits, hipStream_t s);

@@ -172,8 +172,9 @@ __global__ __launch_bounds__(64, kPad ? 1 : 2) void k_verify_sig12(const Fp* ev,
   XStream S = x_stream();
   team_miller_sig12(T, F, ev, n, ci, S, SigFE<SigProgs12>::final_exp_hint_t());
   // parking records: res in fe[idx] (the result overwrites it), t0 in
-  // park[idx]; a padding team (idx >= n) uses spare records park[n + ...]
-  // (park has n + kTeams12 + 1 records). Recomputed at each use.
+  // park[idx]; a padding team (idx >= n) uses the spare records
+  // park[n + 1 + (idx - n)] and park[n + 1 + kTeams12 + (idx - n)] (park has
+  // n + 1 + 2 kTeams12 records, sig12_scalar_offset). Recomputed at each use.
   SigFE<SigProgs12>::team_final_exp_fc_t(T, S, [=](int k) -> uint32_t* {
     const int i = blockIdx.x * kTeams12 + team12_index();
     if (k == 0) return (i < n ? fe + i : park + n + 1 + (i - n))->w;
@@ -189,12 +190,12 @@ __global__ __launch_bounds__(64, kPad ? 1 : 2) void k_verify_sig12(const Fp* ev,
   }
 }
 
-bool sig12_for(bool pad) {
+bool sig12_for(bool pad, size_t n) {
   static const int mode = [] {
     const char* e = getenv("HG_SIG12");
     return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return mode == 1 || (mode == -1 && !pad);
+  return n <= (size_t)kSig12MaxN && (mode == 1 || (mode == -1 && !pad));
 }
 
 // the evaluated lines, then (each 256-byte aligned) the parking records and
@@ -208,7 +209,8 @@ size_t sig12_lines_bytes(int n) { return sig12_scalar_offset(n) + (size_t)n * 2 
 
 void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Fp* ev, Gt* fe,
                           hipStream_t s, bool pad) {
-  if (n <= 0) return;
+  // k_sig_lines indexes 4 n threads in int (callers bound n by kSig12MaxN)
+  if (n <= 0 || n > kSig12MaxN) return;
   Gt* park = (Gt*)((uint8_t*)ev + sig12_park_offset(n));
   Fp* sc = (Fp*)((uint8_t*)ev + sig12_scalar_offset(n));
   k_sig_scalars<<<(n + kLineBlock - 1) / kLineBlock, kLineBlock, 0, s>>>(sigs, flavor, n, sc);

@@ -905,14 +905,14 @@ static int aggregate_device_locked(hg_ctx* c, const hg_request* d_reqs, size_t n
     if (overlap) {
       HG_CHECK(c, ensure_side(ws));
       HG_CHECK(c, ws.gt_fe.ensure(n));
-      if (sig12_for(lane ? lane->pad : true)) HG_CHECK(c, ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
+      if (sig12_for(lane ? lane->pad : true, n)) HG_CHECK(c, ws.sig_lines.ensure(sig12_lines_bytes((int)n)));
     }
     if (overlap) {
       // s:    pairing (decodes its signatures) ............ -> wait -> compare
       // side: wait -> prologue (codes, counters), plan, chunks, combine -> join
       HG_CHECK(c, hipEventRecord(ws.ev_fork, s));
       PhaseTimer t(c, HG_PHASE_VERIFY, s);
-      if (sig12_for(lane ? lane->pad : true))
+      if (sig12_for(lane ? lane->pad : true, n))
         launch_sig_pairing12(d_sigs, c->flavor, (int)n, c->d_lines, (Fp*)ws.sig_lines.p, ws.gt_fe.p, s,
                              lane ? lane->pad : true);
       else
@@ -1560,6 +1560,7 @@ int hg_debug_fp12(hg_ctx* c, int op, const uint8_t* a, const uint8_t* b, size_t 
 
 int hg_sig_pairing_device(hg_ctx* c, const uint8_t* d_sigs, size_t n, uint8_t* d_fe, int kernel, void* stream) {
   if (!c || (n && (!d_sigs || !d_fe)) || n > (size_t)INT32_MAX || kernel < 0 || kernel > 4) return HG_ERR_ARG;
+  if ((kernel == 2 || kernel == 3) && n > (size_t)kSig12MaxN) return HG_ERR_ARG;  // k_sig_lines: 4 n threads in int
   if (n == 0) return HG_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HG_CHECK(c, hipSetDevice(c->device));
@@ -1800,7 +1801,7 @@ int hg_lane_create(hg_ctx* c, size_t max_batch, size_t max_words, int overlap, h
   if (e == hipSuccess) e = w.gt_partial.ensure(chunks);
   if (e == hipSuccess) e = w.gt_y.ensure(n);
   if (e == hipSuccess) e = w.gt_fe.ensure(n);
-  if (e == hipSuccess && sig12_for(true)) e = w.sig_lines.ensure(sig12_lines_bytes((int)n));
+  if (e == hipSuccess && sig12_for(true, n)) e = w.sig_lines.ensure(sig12_lines_bytes((int)n));
   if (e == hipSuccess && l->overlap) e = ensure_side(w);
   if (e != hipSuccess) {
     c->err = std::string("hg_lane_create: ") + hipGetErrorString(e);
@@ -1895,7 +1896,7 @@ int hg_lane_set_pairing_padding(hg_lane* l, int pad) {
   std::lock_guard<std::mutex> g(c->mu);
   // the unpadded lane runs the 12-lane kernel: its evaluated-line workspace
   // at the lane's largest batch now (never grown between batches)
-  if (sig12_for(pad != 0)) {
+  if (sig12_for(pad != 0, l->max_batch)) {
     HG_CHECK(c, hipSetDevice(c->device));
     HG_CHECK(c, hipStreamSynchronize(l->s));
     if (l->ws.side) HG_CHECK(c, hipStreamSynchronize(l->ws.side));

@@ -166,7 +166,7 @@ struct EchoExec : Exec {
 // error, never a crash). Only the bitset words and the signature are read from
 // the slot later, once, at launch, sized by this copy.
 struct Pending {
-  uint32_t slot, chan, msg, msg_gen;
+  uint32_t slot, gen, chan, msg, msg_gen;
   uint32_t offset, bitlen, level_size;
   Clock::time_point seen;
 };
@@ -211,13 +211,30 @@ struct hg_service {
   // adopted[ch] once the dispatcher has swept the ring the handle left
   std::vector<uint8_t> adopted;
   uint32_t seen_orphans = 0;
-  bool w2_policy = true;  // HG_SERVICE_W2=0: the one-wave kernel only
+  // Service-side records (the shared words are client-writable, so nothing
+  // the orphan path frees or releases rests on them alone):
+  //  outstanding[ch]  requests of channel ch taken at intake, not yet finished
+  //  owed_chan[id]    the channel whose ring the dispatcher pushed slot id
+  //                   into (kNone once the slot is taken again), with the
+  //                   slot generation it had at intake (owed_gen[id])
+  static constexpr uint32_t kNone = 0xFFFFFFFFu;
+  std::vector<uint32_t> outstanding;
+  std::vector<uint32_t> owed_chan, owed_gen;
+  // the two-wave latency form for the service's batches: off by default
+  // (HG_SERVICE_W2=1 turns it on). Measured on the config-4 proxy it bought
+  // no throughput and doubled p99 (profiles/r05sy_service_policy_ab.json:
+  // 2.3-2.8 ms on vs 1.2-1.4 ms off, more and smaller batches)
+  bool w2_policy = false;
+#ifdef HG_SERVICE_TESTING
+  uint32_t test_finish_us = 0;  // HG_SERVICE_TEST_FINISH_US
+#endif
   static constexpr int kW2MaxChecks = 2048;  // the latency form's largest batch (bn256_gt.h kSigW2MaxN)
 
   bool intake();
   void complete(int lane, const int32_t* codes, int32_t fail);
   void finish_slots(const Pending* items, size_t n, const int32_t* codes, int32_t fail);
   void free_slot(uint32_t id, uint32_t ch);
+  void maybe_release(uint32_t ch);
   void adopt(uint32_t ch);
   void sweep_orphans();
   void drain();
@@ -240,8 +257,10 @@ bool hg_service::intake() {
       Slot* s = v.slot(id);
       if (s->state.load(std::memory_order_acquire) != kSlotQueued) continue;
       s->state.store(kSlotTaken, std::memory_order_relaxed);
-      Pending p{id, s->chan, s->msg, s->msg_gen, s->offset, s->bitlen, s->level_size, now};
+      Pending p{id, s->gen, s->chan, s->msg, s->msg_gen, s->offset, s->bitlen, s->level_size, now};
       pending.push_back(p);
+      owed_chan[id] = kNone;
+      if (p.chan < outstanding.size()) outstanding[p.chan]++;
       if (p.chan < released.size() && released[p.chan]) {
         released[p.chan]--;
         if (returning) returning--;
@@ -257,30 +276,63 @@ bool hg_service::intake() {
 // dispatcher frees it; the channel is released once it owns no slot
 void hg_service::free_slot(uint32_t id, uint32_t ch) {
   Slot* s = v.slot(id);
+  owed_chan[id] = kNone;
   s->state.store(kSlotFree, std::memory_order_release);
   v.free_bits()[id / 64].fetch_or(1ull << (id % 64), std::memory_order_release);
-  Channel* c = v.chan(ch);
-  if (c->inflight.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-    adopted[ch] = 0;
-    c->used.store(kChanFree, std::memory_order_release);
+  // the client-side count (what a live handle would have decremented),
+  // never below zero whatever a client wrote there
+  std::atomic<uint32_t>& in = v.chan(ch)->inflight;
+  uint32_t x = in.load(std::memory_order_acquire);
+  while (x && !in.compare_exchange_weak(x, x - 1, std::memory_order_acq_rel)) {
   }
+  maybe_release(ch);
+}
+
+// an adopted channel is reusable once the service holds none of its requests
+// (its own count) and no slot of it is claimed but not yet queued (the
+// client-side count: a handle closed mid-submit); a new handle starts reading
+// its ring at the tail published at that point, so it never sees a foreign
+// completion
+void hg_service::maybe_release(uint32_t ch) {
+  if (!adopted[ch] || outstanding[ch] || v.chan(ch)->inflight.load(std::memory_order_acquire)) return;
+#ifdef HG_SERVICE_TESTING
+  // the invariant the race harness checks: nothing pushed to this ring is
+  // left unpublished when the channel goes back to the pool
+  if (touched[ch]) {
+    fprintf(stderr, "hg_service: channel %u released with unpublished completions\n", ch);
+    abort();
+  }
+#endif
+  adopted[ch] = 0;
+  v.chan(ch)->used.store(kChanFree, std::memory_order_release);
 }
 
 // takes over an orphaned channel: the completions pushed after its handle's
-// last drain (ring positions [head, tail)) are freed here
+// last drain (ring positions [head, tail)) are freed here. The pending tail
+// of a batch being finished is published first, so that the positions this
+// walk frees are never published afterwards (a handle opened on
+// the released channel would read them). head and the ring are client-written:
+// a walk longer than the ring is a forged header and frees nothing, and a
+// ring entry is freed only if the dispatcher itself pushed that slot, with
+// that generation, into this channel's ring and it is still Done.
 void hg_service::adopt(uint32_t ch) {
   Channel* c = v.chan(ch);
+  if (touched[ch]) {
+    touched[ch] = 0;
+    c->tail.store(tails[ch], std::memory_order_seq_cst);
+  }
   adopted[ch] = 1;
   const uint32_t cap = v.h->nslots;
   const uint32_t* ring = v.ring(ch);
-  std::vector<uint32_t> ids;
-  for (uint32_t k = c->head; k != tails[ch]; k++) ids.push_back(ring[k % cap]);
-  for (uint32_t id : ids)
-    if (id < cap && v.slot(id)->state.load(std::memory_order_acquire) == kSlotDone) free_slot(id, ch);
-  if (adopted[ch] && c->inflight.load(std::memory_order_acquire) == 0) {
-    adopted[ch] = 0;
-    c->used.store(kChanFree, std::memory_order_release);
-  }
+  const uint32_t head = c->head, dist = tails[ch] - head;
+  if (dist <= cap)
+    for (uint32_t k = 0; k < dist; k++) {
+      const uint32_t id = ring[(head + k) % cap];
+      if (id >= cap || owed_chan[id] != ch) continue;
+      Slot* s = v.slot(id);
+      if (s->state.load(std::memory_order_acquire) == kSlotDone && s->gen == owed_gen[id]) free_slot(id, ch);
+    }
+  maybe_release(ch);
 }
 
 void hg_service::sweep_orphans() {
@@ -297,11 +349,17 @@ void hg_service::finish_slots(const Pending* items, size_t n, const int32_t* cod
   if (n == 0) return;
   const uint32_t cap = v.h->nslots;
   for (size_t i = 0; i < n; i++) {
+#ifdef HG_SERVICE_TESTING
+    // the CPU race harness widens the windows between one completion and the
+    // next and before the tails' publication (service_asan.cpp "race")
+    if (test_finish_us && i) std::this_thread::sleep_for(std::chrono::microseconds(test_finish_us));
+#endif
     const uint32_t id = items[i].slot, ch = items[i].chan;
     Slot* s = v.slot(id);
     s->code = codes ? codes[i] : fail;
     s->state.store(kSlotDone, std::memory_order_release);
     if (ch >= v.h->nchan) continue;
+    if (outstanding[ch]) outstanding[ch]--;
     Channel* c = v.chan(ch);
     if (c->used.load(std::memory_order_acquire) == kChanOrphaned) {
       if (!adopted[ch]) adopt(ch);
@@ -310,10 +368,15 @@ void hg_service::finish_slots(const Pending* items, size_t n, const int32_t* cod
         continue;
       }
     }
+    owed_chan[id] = ch;
+    owed_gen[id] = items[i].gen;
     v.ring(ch)[tails[ch] % cap] = id;
     tails[ch]++;
     touched[ch] = 1;
   }
+#ifdef HG_SERVICE_TESTING
+  if (test_finish_us) std::this_thread::sleep_for(std::chrono::microseconds(test_finish_us));
+#endif
   for (uint32_t ch = 0; ch < v.h->nchan; ch++) {
     if (!touched[ch]) continue;
     touched[ch] = 0;
@@ -434,9 +497,9 @@ void hg_service::launch(int lane) {
       memcpy(w + wo, s->words(), 8ull * nw);
       wo += nw;
     }
-    // the two-wave latency form while the batches in flight leave a SIMD
-    // for each of its waves (padded kernels: one wave per SIMD), else the
-    // one-wave kernel; HG_SERVICE_W2=0 never
+    // with HG_SERVICE_W2=1: the two-wave latency form while the batches in
+    // flight leave a SIMD for each of its waves (padded kernels: one wave per
+    // SIMD), else the one-wave kernel (the default: always)
     const int n = (int)take.size(), one = (n + 3) / 4;
     int used = 0;
     for (const LaneState& o : lanes)
@@ -563,7 +626,13 @@ int create_common(const char* name, const hg_service_config* in, uint32_t nreg, 
   s->touched.assign(cfg.channels, 0);
   s->released.assign(cfg.channels, 0);
   s->adopted.assign(cfg.channels, 0);
+  s->outstanding.assign(cfg.channels, 0);
+  s->owed_chan.assign(cfg.slots, hg_service::kNone);
+  s->owed_gen.assign(cfg.slots, 0);
   s->lanes.resize(cfg.lanes);
+#ifdef HG_SERVICE_TESTING
+  if (const char* e = getenv("HG_SERVICE_TEST_FINISH_US")) s->test_finish_us = (uint32_t)atoi(e);
+#endif
   return HG_OK;
 }
 

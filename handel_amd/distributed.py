@@ -39,12 +39,14 @@ def unpack_verdicts(bits: torch.Tensor, n: int) -> torch.Tensor:
 
 def gather_verdicts(bits: torch.Tensor, world: int, out: List[torch.Tensor] = None) -> List[torch.Tensor]:
     """all_gather of equal-size bitsets (every rank gets every rank's verdicts).
-    With one rank the gather is the identity and copies nothing: the result
-    (and out[0], when `out` is given) IS `bits`, so it changes when the caller
-    rewrites `bits` (bench.py's world-1 step gathers nothing, and says so)."""
+    With one rank and no process group the gather is the identity and copies
+    nothing: the result (and out[0], when `out` is given) IS `bits`, so it
+    changes when the caller rewrites `bits` (bench.py's world-1 step gathers
+    nothing, and says so). With a process group of one rank (bench.py's
+    HG_BENCH_FORCE_PG test hook) the collective runs."""
     import torch.distributed as dist
 
-    if world == 1:  # one rank: the gather is the identity
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):  # the gather is the identity
         if out is None:
             return [bits]
         out[0] = bits

@@ -162,6 +162,14 @@ static double now_s(void) {
   return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
 }
 
+/* one progress line per process phase on stderr (bench.py keeps the tail of
+ * a run that times out, so a stall names the phase it stalled in) */
+static double g_t_start;
+static void stage(const char* who, int p, const char* what) {
+  fprintf(stderr, "[proxy %.3f s] %s %d (pid %d): %s\n", now_s() - g_t_start, who, p, (int)getpid(), what);
+  fflush(stderr);
+}
+
 static uint64_t splitmix(uint64_t* s) {
   uint64_t z = (*s += 0x9e3779b97f4a7c15ull);
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -443,14 +451,18 @@ static void run_context_process(const opts* o, int p, int ready_fd, int start_fd
   memset(&res, 0, sizeof res);
   g_o = o;
   g_p = p;
+  stage("process", p, "forked");
   resolve_gpu(o->lib);
+  stage("process", p, "libhandel_gpu.so loaded");
   const double ts0 = now_s();
   const size_t N = (size_t)o->nreg;
   uint64_t* sk = (uint64_t*)malloc(N * 4 * sizeof(uint64_t));
   uint8_t* reg = (uint8_t*)malloc(N * 128);
   hg_ctx* ctx = setup_context(o, p, reg, sk);
+  stage("process", p, "context, message, registry");
   gen_checks(o, p, sk, 0);
   sign_checks(ctx, p);
+  stage("process", p, "checks signed");
   if (p == 0 && o->dump) {
     char path[4096];
     snprintf(path, sizeof path, "%s/reg.bin", o->dump);
@@ -467,16 +479,19 @@ static void run_context_process(const opts* o, int p, int ready_fd, int start_fd
       exit(4);
     }
     res.prepare_s = now_s() - tp;
+    stage("process", p, "tables prepared");
   }
   if (A.b_create(ctx, (size_t)o->max_batch, (unsigned)o->wait_us, &g_b) != HG_OK) exit(4);
   char c1 = 'r';
   if (write(ready_fd, &c1, 1) != 1) exit(5);
   if (read(start_fd, &c1, 1) != 1) exit(5);
+  stage("process", p, "started");
   pthread_t th[256];
   res.t0 = now_s();
   for (int w = 0; w < o->workers; w++) pthread_create(&th[w], NULL, batcher_worker, (void*)(intptr_t)w);
   for (int w = 0; w < o->workers; w++) pthread_join(th[w], NULL);
   res.t1 = now_s();
+  stage("process", p, "checks done");
   A.b_stats(g_b, &res.batches, &res.requests);
   A.b_destroy(g_b);
   res.in_flight = 1;
@@ -484,6 +499,7 @@ static void run_context_process(const opts* o, int p, int ready_fd, int start_fd
   res.ctx_bytes = A.ctx_bytes(ctx);
   res.rc |= g_fail;
   A.destroy(ctx);
+  stage("process", p, "context destroyed");
   if (write_full(out_fd, &res, sizeof res)) exit(5);
   exit(0);
 }
@@ -758,6 +774,7 @@ int main(int argc, char** argv) {
                     "queues <= 32)\n");
     return 2;
   }
+  g_t_start = now_s();
   workload_map(&o);
   const pid_t me = getpid();
   pid_t pid[16], spid = -1;
@@ -803,6 +820,7 @@ int main(int argc, char** argv) {
     char c;
     if (read_full(ready[p][0], &c, 1)) bad = 1;
   }
+  stage("parent", 0, "every process ready");
   for (int p = 0; p < o.procs; p++) {
     char c = 's';
     if (write(start[p][1], &c, 1) != 1) bad = 1;
@@ -816,11 +834,13 @@ int main(int argc, char** argv) {
       memset(&r[p], 0, sizeof r[p]);
     }
   }
+  stage("parent", 0, "every result in");
   for (int p = 0; p < o.procs; p++) {
     int st = 0;
     waitpid(pid[p], &st, 0);
     if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) bad = 1;
   }
+  stage("parent", 0, "every process exited");
   if (o.daemon) {
     char c = 'q';
     if (write(sstop[1], &c, 1) != 1) bad = 1;

@@ -16,6 +16,14 @@
 //   hostile  4 submitting threads while a fifth rewrites the size fields of
 //            random slot headers continuously: every ticket comes back (its
 //            code may be anything), no bad access
+//   race     a handle closed while the batch holding its last tickets is
+//            being finished (one channel, many rounds at random moments): the
+//            channel is released only once the service holds none of its
+//            slots, and every later handle sees exactly its own tickets
+//   forged   an orphan header forged in shared memory (head far behind the
+//            tail, ring entries naming another channel's finished slots):
+//            the dispatcher neither stalls nor frees the other channel's
+//            slots, whose owner still collects its verdicts
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -230,6 +238,126 @@ static void scenario_hostile(const char* name) {
   hg_service_destroy(s);
 }
 
+static void scenario_race(const char* name) {
+  // one channel, so every round's handle reuses the channel the previous one
+  // closed; the dispatcher pauses 100 us after each completion it pushes
+  // (HG_SERVICE_TEST_FINISH_US), so a close lands between a batch's pushes
+  // and the publication of its tail in many rounds
+  setenv("HG_SERVICE_TEST_FINISH_US", "100", 1);
+  hg_service* s = echo(name, 2, 1, 128, 20, 0, 128, 300);
+  unsetenv("HG_SERVICE_TEST_FINISH_US");
+  CHECK(s);
+  if (!s) return;
+  std::mt19937_64 g(11);
+  uint64_t w[1] = {3};
+  uint8_t sig[64];
+  echo_sig(w, 1, false, sig);
+  hg_request q{0, 64, 64, 0};
+  for (int round = 0; round < 300; round++) {
+    hg_client* c = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hg_client_open(name, &c) != HG_OK) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        CHECK(!"channel never released");
+        hg_service_destroy(s);
+        return;
+      }
+      std::this_thread::yield();
+    }
+    // the previous handles' tickets never show up here: collect this
+    // handle's first ticket and nothing else
+    uint64_t t = 0;
+    CHECK(hg_client_submit(c, kMsg, sizeof kMsg, &q, w, sig, &t) == HG_OK);
+    uint64_t tk[8];
+    int32_t cd[8];
+    const int n = hg_client_wait_any(c, tk, cd, 8, 2000000);
+    CHECK(n == 1 && tk[0] == t && cd[0] == HG_OK);
+    // then several more, and close at a random moment around their batch
+    const int k = 1 + (int)(g() % 6);
+    for (int i = 0; i < k; i++) CHECK(hg_client_submit(c, kMsg, sizeof kMsg, &q, w, sig, &t) == HG_OK);
+    std::this_thread::sleep_for(std::chrono::microseconds(g() % 1200));
+    hg_client_close(c);
+  }
+  // every slot comes back: a fresh handle claims the whole region
+  hg_client* c = nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (hg_client_open(name, &c) != HG_OK && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  CHECK(c);
+  if (c) {
+    std::set<uint64_t> mine, got;
+    for (int i = 0; i < 128; i++) {
+      uint64_t t;
+      CHECK(hg_client_submit(c, kMsg, sizeof kMsg, &q, w, sig, &t) == HG_OK);
+      mine.insert(t);
+    }
+    uint64_t tk[128];
+    int32_t cd[128];
+    while (got.size() < mine.size()) {
+      const int n = hg_client_wait_any(c, tk, cd, 128, 2000000);
+      CHECK(n > 0);
+      if (n <= 0) break;
+      for (int i = 0; i < n; i++) CHECK(mine.count(tk[i]) == 1 && got.insert(tk[i]).second);
+    }
+    hg_client_close(c);
+  }
+  hg_service_destroy(s);
+}
+
+static void scenario_forged(const char* name) {
+  hg_service* s = echo(name, 2, 4, 64, 20, 0, 128, 200);
+  CHECK(s);
+  if (!s) return;
+  hg_client* victim = nullptr;
+  hg_client* other = nullptr;
+  CHECK(hg_client_open(name, &victim) == HG_OK);  // channel 0
+  CHECK(hg_client_open(name, &other) == HG_OK);   // channel 1
+  Region r(name);
+  uint64_t w[1] = {5};
+  uint8_t sig[64];
+  echo_sig(w, 1, false, sig);
+  hg_request q{0, 64, 64, 0};
+  // the victim's tickets finish but stay uncollected
+  std::vector<uint64_t> vt(8);
+  for (auto& t : vt) CHECK(hg_client_submit(victim, kMsg, sizeof kMsg, &q, w, sig, &t) == HG_OK);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r.v.chan(0)->tail.load() < 8 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  CHECK(r.v.chan(0)->tail.load() == 8);
+  // a hostile process forges channel 2 as orphaned: (a) a head ~2^32
+  // positions behind the tail, (b) then ring entries naming the victim's
+  // finished slots
+  Channel* f = r.v.chan(2);
+  f->used.store(kChanOrphaned);
+  f->head = f->tail.load() + 1;
+  r.v.h->orphans.fetch_add(1);
+  r.v.h->doorbell.fetch_add(1);
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  Channel* f3 = r.v.chan(3);
+  uint32_t* ring3 = r.v.ring(3);
+  for (int i = 0; i < 8; i++) ring3[i] = (uint32_t)vt[i];
+  f3->head = 0;
+  f3->tail.store(8);
+  f3->used.store(kChanOrphaned);
+  r.v.h->orphans.fetch_add(1);
+  r.v.h->doorbell.fetch_add(1);
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  // the dispatcher still serves the other channel
+  int32_t code = -1;
+  uint64_t t;
+  CHECK(hg_client_submit(other, kMsg, sizeof kMsg, &q, w, sig, &t) == HG_OK);
+  CHECK(hg_client_wait(other, t, &code) == HG_OK && code == HG_OK);
+  // and the victim's slots were not freed under it: its verdicts are there
+  for (uint64_t x : vt) {
+    CHECK((uint32_t)(x >> 32) == r.v.slot((uint32_t)x)->gen);
+    code = -1;
+    CHECK(hg_client_wait(victim, x, &code) == HG_OK && code == HG_OK);
+  }
+  hg_client_close(victim);
+  hg_client_close(other);
+  hg_service_destroy(s);
+}
+
 int main(int argc, char** argv) {
   char name[96];
   const char* only = argc > 1 ? argv[1] : "";
@@ -244,6 +372,14 @@ int main(int argc, char** argv) {
   if (!*only || !strcmp(only, "hostile")) {
     snprintf(name, sizeof name, "/hg_asan_ho_%d", (int)getpid());
     scenario_hostile(name);
+  }
+  if (!*only || !strcmp(only, "race")) {
+    snprintf(name, sizeof name, "/hg_asan_ra_%d", (int)getpid());
+    scenario_race(name);
+  }
+  if (!*only || !strcmp(only, "forged")) {
+    snprintf(name, sizeof name, "/hg_asan_fo_%d", (int)getpid());
+    scenario_forged(name);
   }
   printf("{\"failures\": %d}\n", failures);
   return failures ? 1 : 0;

@@ -71,3 +71,23 @@ def test_config4_proxy_only_on_a_one_rank_run():
     i = src.index("if want_config4_proxy(rank, world, args):")
     j = src.index('extra["config4_proxy"]')
     assert i < j and "\n        extra" not in src[i:j] and src[j - 12:j] == " " * 12
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_cpu_baseline_on_every_world_size(n):
+    """an N-rank line carries `cpu_baseline` too (rank 0
+    runs it after the timed regions, the other ranks wait at a barrier;
+    bench.cpu_baseline_on_rank0, the function main() uses). Exercised through
+    the real launcher with gloo and the CPU oracle on a tiny workload."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--cpu-probe"],
+                       capture_output=True, text=True, timeout=300, env=_env(HG_BENCH_BACKEND="gloo"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == n
+    cpu = out["cpu_baseline"]
+    assert "error" not in cpu, cpu
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port" and cpu["sample"]
+    # the same call site serves the headline and config 2's lines at any world
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "world == 1 and not args.no_cpu" not in src
+    assert src.count("cpu_baseline_on_rank0(") >= 3

@@ -2,9 +2,11 @@
 
 bench.py's headline (BASELINE config 3, and config 5 with --committees) does
 not run the context's padded submission: it keeps FOUR 4096-request batches
-in flight on four `DeviceLane(pad=False)` lanes of one context — the unpadded
-pairing kernel `k_verify_sig<4, true, false>`, each lane ordered on its own
-stream, nothing synchronised between batches (bench.py `lane_step`). This
+in flight on four `DeviceLane(pad=False)` lanes of one context — unpadded
+lanes run the 12-lane signature pairing (k_sig_scalars + k_sig_lines +
+`k_verify_sig12<false>`, hg_api.cpp sig12_for, bn256_sig12.hip), each lane
+ordered on its own stream, nothing synchronised between batches (bench.py
+`lane_step`). This
 suite runs that path at full size and compares every lane's verdict codes and
 packed bitset with the C restatement of the reference algorithm
 (R.verify_aggregate: processing.go:342-368 verifySignature ->

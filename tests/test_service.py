@@ -362,9 +362,12 @@ def test_follow_policy_counts_only_returning_channels():
 def test_service_trust_boundary_under_asan(tmp_path):
     """tests/native/service_asan.cpp: the service and client sources built for
     the CPU with AddressSanitizer + UBSan (no HIP: the echo executor) and run
-    through three scenarios — slot headers rewritten after queuing, a handle
+    through five scenarios — slot headers rewritten after queuing, a handle
     closed with tickets in flight, a thread rewriting random slots' size
-    fields under load. Any out-of-bounds access aborts the run."""
+    fields under load, handles closed while their last batch is being
+    finished, and a forged orphan header (a head 2^32 positions
+    behind, ring entries naming another channel's slots). Any out-of-bounds
+    access aborts the run."""
     import shutil
 
     gxx = shutil.which("g++")
@@ -376,7 +379,7 @@ def test_service_trust_boundary_under_asan(tmp_path):
             os.path.join(root, "handel_amd", "csrc", "hg_client.cpp"),
             os.path.join(root, "tests", "native", "service_asan.cpp")]
     subprocess.run([gxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
-                    *srcs, "-lpthread", "-o", exe], check=True, capture_output=True, timeout=300)
+                    "-DHG_SERVICE_TESTING", *srcs, "-lpthread", "-o", exe], check=True, capture_output=True, timeout=300)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:verify_asan_link_order=0",
                UBSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)

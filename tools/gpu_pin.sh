@@ -3,6 +3,8 @@
 #  1. the driver's invocation, plain (bench.json);
 #  2. the same invocation under --kernel-trace --stats: its bench line and its
 #     per-kernel averages come from ONE run (bench_traced.json, *_driver_ktrace_stats.csv);
+#     and the per-step device-busy time of its timed region (tools/busy_summary.py:
+#     the union of the kernel intervals inside it / steps -> *_driver_busy.json);
 #  3. PMC passes of the headline alone (HBM bytes, SQ counters), one counter
 #     group per run, and one HBM pass over the config-2 `single` line's
 #     k_verify (its roofline's traffic).
@@ -24,4 +26,5 @@ timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY --kernel-include-regex "$K" -d $OUT/sq -o run -- python3 $H > $OUT/sq.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_verify<" -d $OUT/single_fetch -o run -- python3 $S > $OUT/single_fetch.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_verify<" -d $OUT/single_write -o run -- python3 $S > $OUT/single_write.log 2>&1 &&
-python3 tools/rocpd_summary.py $OUT $OUT/${R}_driver && rm -f $OUT/*/*.db
+python3 tools/rocpd_summary.py $OUT $OUT/${R}_driver &&
+python3 tools/busy_summary.py $OUT/ktrace $OUT/bench_traced.json $OUT/${R}_driver_busy.json && rm -f $OUT/*/*.db
