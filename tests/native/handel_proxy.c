@@ -70,6 +70,20 @@
 static const uint8_t kMsg[] = "Everything that is beautiful and noble is the product of reason and calculation.";
 #define MSG_LEN (sizeof kMsg - 1) /* lib.Message, simul/lib/config.go:37 */
 
+/* A forked child ends with _exit after flushing stdio: its atexit handlers
+ * and static destructors are the PARENT's registrations, copied by fork. A
+ * profiler's tool library preloaded into the parent (rocprofv3) registers its
+ * finalizer there; run in two or more children at once it aborts inside
+ * __cxa_finalize and its signal handler then never returns, so the parent's
+ * waitpid hung (the contexts model under rocprofv3, diagnosed
+ * from this proxy's stage log, tools/proxy_prof.py). The children release
+ * their GPU contexts explicitly before this (hg_destroy); the kernel driver
+ * reclaims the rest of a process at exit, as for any process. */
+static void child_exit(int code) {
+  fflush(NULL);
+  _exit(code);
+}
+
 /* ---------------------------------------------------------------- the C ABIs, resolved after fork */
 static struct {
   int (*create)(int, int, hg_ctx**);
@@ -108,7 +122,7 @@ static void* open_lib(const char* path) {
   void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
   if (!h) {
     fprintf(stderr, "dlopen %s: %s\n", path, dlerror());
-    exit(3);
+    child_exit(3);
   }
   return h;
 }
@@ -117,7 +131,7 @@ static void* open_lib(const char* path) {
     *(void**)(&S.field) = dlsym(h, name);                  \
     if (!S.field) {                                        \
       fprintf(stderr, "missing symbol %s\n", name);        \
-      exit(3);                                             \
+      child_exit(3);                                             \
     }                                                      \
   } while (0)
 
@@ -379,7 +393,7 @@ static hg_ctx* setup_context(const opts* o, int p, uint8_t* reg, uint64_t* sk) {
   hg_ctx* ctx = NULL;
   if (A.create(0, HG_FLAVOR_GO, &ctx) != HG_OK) {
     fprintf(stderr, "proc %d: hg_create failed\n", p);
-    exit(4);
+    child_exit(4);
   }
   if (o->level != -1) A.set_level(ctx, o->level);
   if (o->budget_mb >= 0) A.set_budget(ctx, (size_t)o->budget_mb << 20);
@@ -392,7 +406,7 @@ static hg_ctx* setup_context(const opts* o, int p, uint8_t* reg, uint64_t* sk) {
   free(skb);
   if (rc != HG_OK) {
     fprintf(stderr, "proc %d: setup rc %d: %s\n", p, rc, A.last_error(ctx));
-    exit(4);
+    child_exit(4);
   }
   return ctx;
 }
@@ -402,7 +416,7 @@ static void sign_checks(hg_ctx* ctx, int p) {
   int rc = A.sign(ctx, W_.agg_sk + (size_t)p * nchk * 32, nchk, W_.sigs + (size_t)p * nchk * 64);
   if (rc != HG_OK) {
     fprintf(stderr, "proc %d: sign rc %d: %s\n", p, rc, A.last_error(ctx));
-    exit(4);
+    child_exit(4);
   }
 }
 
@@ -476,15 +490,15 @@ static void run_context_process(const opts* o, int p, int ready_fd, int start_fd
     const double tp = now_s();
     if (A.prepare(ctx) != HG_OK) {
       fprintf(stderr, "proc %d: prepare: %s\n", p, A.last_error(ctx));
-      exit(4);
+      child_exit(4);
     }
     res.prepare_s = now_s() - tp;
     stage("process", p, "tables prepared");
   }
-  if (A.b_create(ctx, (size_t)o->max_batch, (unsigned)o->wait_us, &g_b) != HG_OK) exit(4);
+  if (A.b_create(ctx, (size_t)o->max_batch, (unsigned)o->wait_us, &g_b) != HG_OK) child_exit(4);
   char c1 = 'r';
-  if (write(ready_fd, &c1, 1) != 1) exit(5);
-  if (read(start_fd, &c1, 1) != 1) exit(5);
+  if (write(ready_fd, &c1, 1) != 1) child_exit(5);
+  if (read(start_fd, &c1, 1) != 1) child_exit(5);
   stage("process", p, "started");
   pthread_t th[256];
   res.t0 = now_s();
@@ -500,8 +514,8 @@ static void run_context_process(const opts* o, int p, int ready_fd, int start_fd
   res.rc |= g_fail;
   A.destroy(ctx);
   stage("process", p, "context destroyed");
-  if (write_full(out_fd, &res, sizeof res)) exit(5);
-  exit(0);
+  if (write_full(out_fd, &res, sizeof res)) child_exit(5);
+  child_exit(0);
 }
 
 /* ---------------------------------------------------------------- model 1: the verifier service */
@@ -537,7 +551,7 @@ static void run_server(const opts* o, pid_t parent, int ready_fd, int stop_fd, i
     res.setup_s = now_s() - ts0;
     if (A.s_create_echo(name, &cfg, (uint32_t)o->nreg, (uint32_t)o->echo_us, &svc) != HG_OK) {
       fprintf(stderr, "server: hg_service_create_echo failed\n");
-      exit(4);
+      child_exit(4);
     }
   } else {
     uint64_t* sk = (uint64_t*)malloc(N * 4 * sizeof(uint64_t));
@@ -560,17 +574,17 @@ static void run_server(const opts* o, pid_t parent, int ready_fd, int stop_fd, i
       const double tp = now_s();
       if (A.prepare(ctx) != HG_OK) {
         fprintf(stderr, "server: prepare: %s\n", A.last_error(ctx));
-        exit(4);
+        child_exit(4);
       }
       res.prepare_s = now_s() - tp;
     }
     if (A.s_create(ctx, name, &cfg, &svc) != HG_OK) {
       fprintf(stderr, "server: hg_service_create failed: %s\n", A.last_error(ctx));
-      exit(4);
+      child_exit(4);
     }
   }
   char c1 = 'r';
-  if (write(ready_fd, &c1, 1) != 1) exit(5);
+  if (write(ready_fd, &c1, 1) != 1) child_exit(5);
   if (read(stop_fd, &c1, 1) != 1) res.rc = 1; /* the parent: every client is done */
   A.s_stats(svc, &res.batches, &res.requests, &res.in_flight);
   A.s_destroy(svc);
@@ -579,8 +593,8 @@ static void run_server(const opts* o, pid_t parent, int ready_fd, int stop_fd, i
     res.ctx_bytes = A.ctx_bytes(ctx);
     A.destroy(ctx);
   }
-  if (write_full(out_fd, &res, sizeof res)) exit(5);
-  exit(0);
+  if (write_full(out_fd, &res, sizeof res)) child_exit(5);
+  child_exit(0);
 }
 
 typedef struct {
@@ -665,12 +679,12 @@ static void run_client_process(const opts* o, int p, pid_t parent, int ready_fd,
     pa[w].fail = 0;
     if (C.open(name, &pa[w].cl) != HG_OK) {
       fprintf(stderr, "client %d: hg_client_open(%s) failed\n", p, name);
-      exit(4);
+      child_exit(4);
     }
   }
   char c1 = 'r';
-  if (write(ready_fd, &c1, 1) != 1) exit(5);
-  if (read(start_fd, &c1, 1) != 1) exit(5);
+  if (write(ready_fd, &c1, 1) != 1) child_exit(5);
+  if (read(start_fd, &c1, 1) != 1) child_exit(5);
   pthread_t th[256];
   res.t0 = now_s();
   for (int w = 0; w < o->workers; w++) pthread_create(&th[w], NULL, poller, &pa[w]);
@@ -681,8 +695,8 @@ static void run_client_process(const opts* o, int p, pid_t parent, int ready_fd,
     C.close(pa[w].cl);
   }
   res.requests = W_.nchk;
-  if (write_full(out_fd, &res, sizeof res)) exit(5);
-  exit(0);
+  if (write_full(out_fd, &res, sizeof res)) child_exit(5);
+  child_exit(0);
 }
 
 /* ---------------------------------------------------------------- parent */
