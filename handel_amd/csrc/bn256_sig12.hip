@@ -190,6 +190,174 @@ __global__ __launch_bounds__(64, kPad ? 1 : 2) void k_verify_sig12(const Fp* ev,
   }
 }
 
+// ---------------------------------------------------------------- split form
+// The same chain in three kernels, so that the one Fp inversion per check
+// (the norm of f down to Fp, t12_inv_norm's Bernstein-Yang inversion: 4.3 %
+// of k_verify_sig12's VALU instructions and 13 % of its SALU ones, measured
+// by dropping it, profiles/r06p_inv_probe.json) is done for 256 checks at
+// a time instead of once per wave:
+//   k_sig12_miller  the Miller loop and the norm N = f conj(f) (bn256_sigfe.h
+//                   fe_t_norm), then t12_inv_norm up to d (t12_inv_norm_terms):
+//                   f -> fe[c], the terms -> hand[c], n = |d|^2 -> nrm[c]
+//   k_sig12_ninv    nrm[c]^-1 for every check, by a product tree per 256
+//                   checks and ONE inversion at its root
+//   k_sig12_fe      f back into the team region, N^-1 from the terms and
+//                   n^-1 (t12_inv_norm_finish), the rest of the chain
+// The values are the monolithic kernel's, bit for bit: n^-1 is the unique
+// canonical inverse either way, and every other operation is the same.
+struct SigHand {
+  Fp v[8];  // t0, t1, t2, d (x, y each)
+};
+
+template <bool kPad>
+__global__ __launch_bounds__(64, kPad ? 1 : 2) void k_sig12_miller(const Fp* ev, int n, Gt* fe, SigHand* hand,
+                                                                   Fp* nrm) {
+  constexpr int kWords = kSigTTeamElems * 10;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams12 * kWords];
+  __builtin_amdgcn_s_setprio(3);
+  if constexpr (kPad) asm volatile("" ::: "v255", "a0");
+  Team T = make_team12(lds, kWords);
+  uint32_t* F = T.base + kSigTRegBase * 10;
+  const int idx = blockIdx.x * kTeams12 + team12_index();
+  const bool valid = idx < n;
+  const int ci = valid ? idx : n - 1;
+  XStream S = x_stream();
+  team_miller_sig12(T, F, ev, n, ci, S, xh<ISqr12T>());
+  SigFE<SigProgs12>::fe_t_norm(T, S, xh_none());
+  NormTerms o;
+  Fp nr;
+  t12_inv_norm_terms(T, S_B, o, nr);
+  Fp v;
+  ld_fp_a8(v, slot(T, S_F) + T.e * 10);
+  if (valid && T.active) {
+    uint2* dst = (uint2*)__builtin_assume_aligned(fe[idx].w + 10 * T.e, 8);
+#pragma unroll
+    for (int i = 0; i < 5; i++) dst[i] = make_uint2(v.l[2 * i], v.l[2 * i + 1]);
+  }
+  // lane tl < 8 stores term value tl, lane 8 the norm (team-uniform values)
+  if (valid && T.tl < 9) {
+    Fp2 pick;  // (selects on values, not on member references: no scratch)
+    f2_sel(pick, T.tl < 6, o.t2, o.d);
+    f2_sel(pick, T.tl < 4, o.t1, pick);
+    f2_sel(pick, T.tl < 2, o.t0, pick);
+    Fp w;
+    fp_sel(w, (T.tl & 1) == 0, pick.x, pick.y);
+    fp_sel(w, T.tl == 8, nr, w);
+    uint2* dst = (uint2*)__builtin_assume_aligned(T.tl == 8 ? nrm[idx].l : hand[idx].v[T.tl].l, 8);
+#pragma unroll
+    for (int i = 0; i < 5; i++) dst[i] = make_uint2(w.l[2 * i], w.l[2 * i + 1]);
+  }
+}
+
+// ninv[c] = nrm[c]^-1 (0 for 0: never the case for a Miller value, whose
+// lines all have the coefficient 1 at w^3, so f and its norms are nonzero;
+// guarded so one value cannot spoil the other 255). Per block of 256 checks:
+// a product tree in LDS (8 levels), one fp_inv at the root, the inverses
+// back down (inv(left) = inv(parent) right, inv(right) = inv(parent) left).
+static constexpr int kInvBlock = 256;
+__global__ __launch_bounds__(kInvBlock) void k_sig12_ninv(const Fp* nrm, int n, Fp* ninv) {
+  // levels of the tree: the 256 leaves at 0, then 128 nodes at 256, 64 at
+  // 384, ..., the root at 510
+  __shared__ Fp tree[2 * kInvBlock];
+  const int t = threadIdx.x;
+  const int c = blockIdx.x * kInvBlock + t;
+  Fp x, one;
+  fp_one(one);
+  x = one;
+  const bool use = c < n && !fp_is_zero(nrm[c]);
+  if (use) x = nrm[c];
+  tree[t] = x;
+  __syncthreads();
+  int off = 0;  // the level of 2 sz nodes being multiplied pairwise
+  for (int sz = kInvBlock / 2; sz >= 1; sz >>= 1) {
+    if (t < sz) fp_mul(tree[off + 2 * sz + t], tree[off + 2 * t], tree[off + 2 * t + 1]);
+    off += 2 * sz;
+    __syncthreads();
+  }
+  // off: the root's index
+  if (t == 0) fp_inv(tree[off], tree[off]);
+  __syncthreads();
+  for (int sz = 1; sz <= kInvBlock / 2; sz <<= 1) {  // down: the 2 sz children of the level of sz nodes at off
+    const int child = off - 2 * sz;
+    Fp pinv, sib;
+    if (t < 2 * sz) {
+      pinv = tree[off + (t >> 1)];
+      sib = tree[child + (t ^ 1)];
+    }
+    __syncthreads();
+    if (t < 2 * sz) fp_mul(tree[child + t], pinv, sib);
+    off = child;
+    __syncthreads();
+  }
+  if (c < n) {
+    Fp z;
+    fp_zero(z);
+    fp_sel(x, use, tree[t], z);
+    ninv[c] = x;
+  }
+}
+
+template <bool kPad>
+__global__ __launch_bounds__(64, kPad ? 1 : 2) void k_sig12_fe(int n, Gt* fe, Gt* park, const SigHand* hand,
+                                                               const Fp* ninv) {
+  constexpr int kWords = kSigTTeamElems * 10;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams12 * kWords];
+  __builtin_amdgcn_s_setprio(3);
+  if constexpr (kPad) asm volatile("" ::: "v255", "a0");
+  Team T = make_team12(lds, kWords);
+  uint32_t* F = T.base + kSigTRegBase * 10;
+  const int idx = blockIdx.x * kTeams12 + team12_index();
+  const bool valid = idx < n;
+  const int ci = valid ? idx : n - 1;
+  XStream S = x_stream();
+  // the registers the programs read, f into slot F
+  if (T.tl == 0) {
+    Fp zero, one;
+    fp_zero(zero);
+    fp_one(one);
+    st_fp(F + R_ZERO * 10, zero);
+    st_fp(F + R_ONE * 10, one);
+  }
+  {
+    const uint2* src = (const uint2*)__builtin_assume_aligned(fe[ci].w + 10 * T.e, 8);
+    uint32_t v[10];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const uint2 x = src[i];
+      v[2 * i] = x.x;
+      v[2 * i + 1] = x.y;
+    }
+    if (T.active) st_fp_a8(slot(T, S_F) + T.e * 10, v);
+  }
+  team_sync();
+  t12_conj(T, S_D, S_F);
+  NormTerms o;
+  const SigHand& h = hand[ci];
+  o.t0.x = h.v[0];
+  o.t0.y = h.v[1];
+  o.t1.x = h.v[2];
+  o.t1.y = h.v[3];
+  o.t2.x = h.v[4];
+  o.t2.y = h.v[5];
+  o.d.x = h.v[6];
+  o.d.y = h.v[7];
+  t12_inv_norm_finish(T, S_B, o, ninv[ci]);
+  // parking as k_verify_sig12
+  SigFE<SigProgs12>::fe_t_rest(T, S, [=](int k) -> uint32_t* {
+    const int i = blockIdx.x * kTeams12 + team12_index();
+    if (k == 0) return (i < n ? fe + i : park + n + 1 + (i - n))->w;
+    return (i < n ? park + i : park + n + 1 + kTeams12 + (i - n))->w;
+  });
+  team_sync();
+  Fp v;
+  ld_fp_a8(v, slot(T, S_F) + T.e * 10);
+  if (valid && T.active) {
+    uint2* dst = (uint2*)__builtin_assume_aligned(fe[idx].w + 10 * T.e, 8);
+#pragma unroll
+    for (int i = 0; i < 5; i++) dst[i] = make_uint2(v.l[2 * i], v.l[2 * i + 1]);
+  }
+}
+
 bool sig12_for(bool pad, size_t n) {
   static const int mode = [] {
     const char* e = getenv("HG_SIG12");
@@ -198,24 +366,48 @@ bool sig12_for(bool pad, size_t n) {
   return n <= (size_t)kSig12MaxN && (mode == 1 || (mode == -1 && !pad));
 }
 
-// the evaluated lines, then (each 256-byte aligned) the parking records and
-// the signatures' scalars
+// the split form (k_sig12_miller, k_sig12_ninv, k_sig12_fe) unless HG_SIG12_SPLIT=0
+static bool sig12_split() {
+  static const bool on = [] {
+    const char* e = getenv("HG_SIG12_SPLIT");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// the evaluated lines, then (each 256-byte aligned) the parking records, the
+// signatures' scalars, and the split form's hand-over records and norms
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 static size_t sig12_park_offset(int n) { return align256((size_t)n * kNumLines * 4 * sizeof(Fp)); }
 static size_t sig12_scalar_offset(int n) {
   return sig12_park_offset(n) + align256((size_t)(n + 1 + 2 * kTeams12) * sizeof(Gt));
 }
-size_t sig12_lines_bytes(int n) { return sig12_scalar_offset(n) + (size_t)n * 2 * sizeof(Fp); }
+static size_t sig12_hand_offset(int n) { return sig12_scalar_offset(n) + align256((size_t)n * 2 * sizeof(Fp)); }
+static size_t sig12_norm_offset(int n) { return sig12_hand_offset(n) + align256((size_t)n * sizeof(SigHand)); }
+static size_t sig12_ninv_offset(int n) { return sig12_norm_offset(n) + align256((size_t)n * sizeof(Fp)); }
+size_t sig12_lines_bytes(int n) { return sig12_ninv_offset(n) + (size_t)n * sizeof(Fp); }
 
 void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Fp* ev, Gt* fe,
                           hipStream_t s, bool pad) {
   // k_sig_lines indexes 4 n threads in int (callers bound n by kSig12MaxN)
   if (n <= 0 || n > kSig12MaxN) return;
-  Gt* park = (Gt*)((uint8_t*)ev + sig12_park_offset(n));
-  Fp* sc = (Fp*)((uint8_t*)ev + sig12_scalar_offset(n));
+  uint8_t* base = (uint8_t*)ev;
+  Gt* park = (Gt*)(base + sig12_park_offset(n));
+  Fp* sc = (Fp*)(base + sig12_scalar_offset(n));
   k_sig_scalars<<<(n + kLineBlock - 1) / kLineBlock, kLineBlock, 0, s>>>(sigs, flavor, n, sc);
   k_sig_lines<<<dim3((4 * n + kLineBlock - 1) / kLineBlock, kNumLines), kLineBlock, 0, s>>>(sc, n, tab, ev);
   const int blocks = (n + kTeams12 - 1) / kTeams12;
+  if (sig12_split()) {
+    SigHand* hand = (SigHand*)(base + sig12_hand_offset(n));
+    Fp* nrm = (Fp*)(base + sig12_norm_offset(n));
+    Fp* ninv = (Fp*)(base + sig12_ninv_offset(n));
+    if (pad) k_sig12_miller<true><<<blocks, 64, 0, s>>>(ev, n, fe, hand, nrm);
+    else k_sig12_miller<false><<<blocks, 64, 0, s>>>(ev, n, fe, hand, nrm);
+    k_sig12_ninv<<<(n + kInvBlock - 1) / kInvBlock, kInvBlock, 0, s>>>(nrm, n, ninv);
+    if (pad) k_sig12_fe<true><<<blocks, 64, 0, s>>>(n, fe, park, hand, ninv);
+    else k_sig12_fe<false><<<blocks, 64, 0, s>>>(n, fe, park, hand, ninv);
+    return;
+  }
   if (pad) k_verify_sig12<true><<<blocks, 64, 0, s>>>(ev, n, fe, park);
   else k_verify_sig12<false><<<blocks, 64, 0, s>>>(ev, n, fe, park);
 }

@@ -147,10 +147,22 @@ struct SigFE {
   // kernel can recompute the addresses instead of holding them in registers
   template <class Park>
   HG_DEV static void team_final_exp_fc_t(const Team& T, XStream& S, Park park) {
+    fe_t_norm(T, S, fe_t_rest_hint());
+    t12_inv_norm(T, S_B);  // N^-1
+    fe_t_rest(T, S, park);
+  }
+  // the chain's first part, up to the norm: D = conj(f), B = N = f conj(f)
+  // (the split kernels of bn256_sig12.hip end here and invert the norms of a
+  // whole batch at once)
+  HG_DEV static void fe_t_norm(const Team& T, XStream& S, XHint h) {
     // easy part: res = f^((p^6 - 1)(p^2 + 1)), f^-1 = conj(f) / (f conj(f))
     t12_conj(T, S_D, S_F);
-    IMul12S<S_B, S_F, S_D>::run(T, S, xh<IMul12S<S_A, S_D, S_B>>());  // N = f conj(f)
-    t12_inv_norm(T, S_B);                                              // N^-1
+    IMul12S<S_B, S_F, S_D>::run(T, S, h);  // N = f conj(f)
+  }
+  HG_DEV static constexpr XHint fe_t_rest_hint() { return xh<IMul12S<S_A, S_D, S_B>>(); }
+  // the rest, with f in F, conj(f) in D and N^-1 in B
+  template <class Park>
+  HG_DEV static void fe_t_rest(const Team& T, XStream& S, Park park) {
     IMul12S<S_A, S_D, S_B>::run(T, S, xh<IMul12S<S_F, S_B, S_A>>());  // A = f^-1
     t12_conj(T, S_B, S_F);
     IMul12S<S_F, S_B, S_A>::run(T, S, xh<IMul12S<S_F, S_F, S_A>>());  // f^(p^6 - 1)

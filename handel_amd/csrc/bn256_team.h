@@ -554,12 +554,105 @@ HG_DEV void t12_inv_norm(const Team& T, int s2) {
   f2_add(d, w0, w1);
   f2_mul_xi(d, d);
   f2_add(d, d, w2);
+#ifndef HG_PROBE_NOINV  // timing probe only (wrong values): the inversion's share of a pairing kernel
   f2_inv(d, d);
+#endif
   // element e of N^-1: component comp of t_m d^-1 (m = k / 2), zero for odd k
   const int m = T.k >> 1;
   Fp2 tm;
   f2_sel(tm, m == 0, t0, m == 1 ? t1 : t2);
   // x (imag) = tm.x d.y + tm.y d.x; y (real) = tm.y d.y - tm.x d.x
+  Fp a1, b1, ntx;
+  fp_neg_loose(ntx, tm.x);
+  fp_sel(a1, T.comp != 0, tm.y, tm.x);
+  fp_sel(b1, T.comp != 0, ntx, tm.y);
+  Acc acc;
+  acc_zero(acc);
+  acc_mad(acc, a1, d.y);
+  acc_mad(acc, b1, d.x);
+  Fp e, z;
+  acc_reduce(e, acc);
+  fp_zero(z);
+  fp_sel(e, (T.k & 1) != 0, z, e);
+  team_sync(T);
+  if (T.active) st_fp(N + T.e * 10, e);
+  team_sync(T);
+}
+
+// t12_inv_norm in two halves around its one Fp inversion, for kernels that
+// invert the norms of a whole batch of checks at once (bn256_sig12.hip: one
+// batched inversion per 256 checks instead of one Bernstein-Yang inversion
+// per wave, 4.3 % of the 12-lane pairing kernel's VALU instructions,
+// profiles/r06p_inv_probe.json). _terms runs t12_inv_norm up to d (the
+// adjugate's terms t0, t1, t2 and d, team-uniform, every lane holds them) and
+// returns n = |d|^2 as f2_inv forms it; _finish, given n^-1, writes N^-1
+// into slot s2 exactly as t12_inv_norm does (the same products in the same
+// order: identical canonical values).
+struct NormTerms {
+  Fp2 t0, t1, t2, d;
+};
+HG_DEV void t12_inv_norm_terms(const Team& T, int s2, NormTerms& o, Fp& nrm) {
+  uint32_t* N = slot(T, s2);
+  Fp2 c0, c1, c2;
+  ld_f2(c0, N, 0);
+  ld_f2(c1, N, 2);
+  ld_f2(c2, N, 4);
+  const int j = T.tl < 3 ? T.tl : 2;
+  Fp2 X, Y, Z, u, v, t;
+  f2_sel(X, j == 0, c0, j == 1 ? c2 : c1);
+  f2_sel(Y, j == 0, c1, c0);
+  f2_sel(Z, j == 1, c1, c2);
+  f2_sqr(u, X);
+  f2_mul(v, Y, Z);
+  Fp2 xu, xv;
+  f2_mul_xi(xu, u);
+  f2_mul_xi(xv, v);
+  f2_sel(u, j == 1, xu, u);
+  f2_sel(v, j == 0, xv, v);
+  f2_sub(t, u, v);
+  team_sync(T);
+  if (T.tl < 3) {
+    st_fp(N + (4 * j + 2) * 10, t.x);
+    st_fp(N + (4 * j + 3) * 10, t.y);
+  }
+  team_sync(T);
+  ld_f2(o.t0, N, 1);
+  ld_f2(o.t1, N, 3);
+  ld_f2(o.t2, N, 5);
+  Fp2 P, Q, w;
+  f2_sel(P, j == 0, c2, j == 1 ? c1 : c0);
+  f2_sel(Q, j == 0, o.t1, j == 1 ? o.t2 : o.t0);
+  f2_mul(w, P, Q);
+  team_sync(T);
+  if (T.tl < 3) {
+    st_fp(N + (4 * j + 2) * 10, w.x);
+    st_fp(N + (4 * j + 3) * 10, w.y);
+  }
+  team_sync(T);
+  Fp2 w0, w1, w2;
+  ld_f2(w0, N, 1);
+  ld_f2(w1, N, 3);
+  ld_f2(w2, N, 5);
+  f2_add(o.d, w0, w1);
+  f2_mul_xi(o.d, o.d);
+  f2_add(o.d, o.d, w2);
+  Acc acc;  // f2_inv's norm
+  acc_zero(acc);
+  acc_sqr(acc, o.d.x);
+  acc_sqr(acc, o.d.y);
+  acc_reduce(nrm, acc);
+}
+HG_DEV void t12_inv_norm_finish(const Team& T, int s2, const NormTerms& o, const Fp& ninv) {
+  uint32_t* N = slot(T, s2);
+  Fp2 d;  // d^-1, as f2_inv
+  Fp ndx;
+  fp_neg(ndx, o.d.x);
+  fp_mul(d.x, ndx, ninv);
+  fp_mul(d.y, o.d.y, ninv);
+  const int m = T.k >> 1;
+  Fp2 tm;  // (selects on values: a select between member references spills to scratch)
+  f2_sel(tm, m == 1, o.t1, o.t2);
+  f2_sel(tm, m == 0, o.t0, tm);
   Fp a1, b1, ntx;
   fp_neg_loose(ntx, tm.x);
   fp_sel(a1, T.comp != 0, tm.y, tm.x);

@@ -194,3 +194,53 @@ def test_pairing_kernels_give_identical_fe_values(engine, engine_cf):
             v = outs[0][:480].view(np.uint32).reshape(12, 10)
             nz = [e for e in range(12) if v[e].any()]
             assert nz == [1], (eng.flavor_name, n, nz, v[:2].tolist())
+
+
+_MONO_CHILD = r"""
+import os, sys
+sys.path.insert(0, os.environ["HG_ROOT"])
+import numpy as np, torch
+import bench
+from handel_amd.engine import Engine
+dev = torch.device("cuda", 0)
+out = []
+for flavor in ("go", "cf"):
+    eng = Engine(device=0, flavor=flavor)
+    assert eng.set_message(bench.LIB_MESSAGE) == 0
+    for n in (7, 1029):
+        sigs = bytearray(eng.sign(bench.seeded_scalars(n, 1900 + n)))
+        sigs[64:128] = bytes(64)
+        d = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
+        for k in (2, 3):
+            fe = torch.full((n * 480,), 0x5A, dtype=torch.uint8, device=dev)
+            eng.sig_pairing_device(d.data_ptr(), n, fe.data_ptr(), k, torch.cuda.current_stream(dev).cuda_stream)
+            torch.cuda.synchronize(dev)
+            out.append(fe.cpu().numpy())
+    eng.close()
+np.save(sys.argv[1], np.concatenate(out))
+"""
+
+
+def test_split_sig12_matches_the_monolithic_kernel(tmp_path):
+    """The 12-lane pairing in three kernels (k_sig12_miller, the batched norm
+    inversion k_sig12_ninv, k_sig12_fe: the default) and in one
+    (k_verify_sig12, HG_SIG12_SPLIT=0) write byte-identical FE values, padded
+    and unpadded, both flavors, ragged n (a 1029-check batch spans five
+    inversion blocks, the last one partly empty), with a point at infinity in
+    the batch. Each form runs in a child process (the switch is read once per
+    process)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    got = {}
+    for split in ("1", "0"):
+        path = str(tmp_path / f"fe_{split}.npy")
+        env = dict(os.environ, HG_SIG12_SPLIT=split, HG_ROOT=root)
+        r = subprocess.run([sys.executable, "-c", _MONO_CHILD, path], capture_output=True, text=True, timeout=240,
+                           env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        got[split] = np.load(path)
+    assert got["1"].size == 2 * 2 * (7 + 1029) * 480
+    assert np.array_equal(got["1"], got["0"])
