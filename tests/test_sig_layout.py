@@ -78,6 +78,8 @@ def _to_python(body):
             m = re.match(r"(ICycS|ICyc0S)<S_(\w), S_(\w)>::run\(.*\)$", s)
             if m:
                 return f"sqr('{m.group(2)}', '{m.group(3)}')"
+            if s == "handover()":
+                return s
             m = re.match(r"t12_pow_v_s<S_(\w), S_(\w), S_(\w)>\(.*\)$", s)
             if m:
                 return f"powv('{m.group(1)}', '{m.group(2)}', '{m.group(3)}')"
@@ -129,14 +131,41 @@ def _to_python(body):
 
 import pytest  # noqa: E402
 
+SIGFE = os.path.join(CSRC, "bn256_sigfe.h")
 
-@pytest.mark.parametrize("layout,slots_used", [("s", "FABCDEG"), ("t", "FABCD")])
-def test_final_exp_layout_matches_oracle(layout, slots_used):
+
+def _t_parts():
+    """layout T's chain in its two parts (fe_t_norm: up to the norm N in B;
+    fe_t_rest: from N^-1 in B on), as the split kernels run them."""
+    return _body(SIGFE, "HG_DEV static void fe_t_norm("), _body(SIGFE, "HG_DEV static void fe_t_rest(")
+
+
+def _fc_source(layout):
+    body = _body(SIGFE, f"HG_DEV static void team_final_exp_fc_{layout}(")
+    if layout == "t":  # the monolithic kernel calls the two parts around t12_inv_norm
+        norm, rest = _t_parts()
+        body = re.sub(r"fe_t_norm\(T, S, [^;]*\);", lambda m: norm, body)
+        assert "fe_t_rest(T, S, park);" in body
+        body = body.replace("fe_t_rest(T, S, park);", rest)
+    return _to_python(body)
+
+
+@pytest.mark.parametrize("layout,slots_used,split", [("s", "FABCDEG", False), ("t", "FABCD", False),
+                                                     ("t", "FABCD", True)])
+def test_final_exp_layout_matches_oracle(layout, slots_used, split):
     """layout s: k_verify_sig's seven slots; layout t: k_verify_sig12's five
-    slots, two values parked in HBM (t12_park / t12_unpark)."""
-    fc_src = _to_python(_body(os.path.join(CSRC, "bn256_sigfe.h"),
-                              f"HG_DEV static void team_final_exp_fc_{layout}("))
-    pow_src = _to_python(_body(os.path.join(CSRC, "bn256_sigfe.h"), "HG_DEV static void t12_pow_v_s("))
+    slots, two values parked in HBM (t12_park / t12_unpark). split: the
+    three-kernel form (bn256_sig12.hip k_sig12_miller / k_sig12_fe): fe_t_norm
+    in the first kernel, then a fresh team region in the last one holding only
+    what k_sig12_fe rebuilds — f in F, conj(f) in D, N^-1 in B (from the
+    handed-over terms and the batched inverse), garbage in every other slot —
+    and fe_t_rest from there."""
+    if split:
+        norm, rest = _t_parts()
+        fc_src = _to_python(norm) + "\nhandover()\n" + _to_python(rest)
+    else:
+        fc_src = _fc_source(layout)
+    pow_src = _to_python(_body(SIGFE, "HG_DEV static void t12_pow_v_s("))
     rng = random.Random(5)
     f = [(rng.randrange(O.P), rng.randrange(O.P)) for _ in range(6)]
     slots = {}
@@ -180,6 +209,17 @@ def test_final_exp_layout_matches_oracle(layout, slots_used):
         assert slots[d] == O.f12_pow(slots[sa], V), "t12_pow_v_s"
 
     env["powv"] = powv
+
+    def handover():
+        n_inv = O.f12_inv(slots["B"])
+        f_val = slots["F"]
+        for s in slots_used:  # a new kernel's team region
+            slots[s] = O.f12_pow(f, rng.randrange(2, 1000))
+        slots["F"] = f_val
+        slots["D"] = O.f12_conj(f_val)
+        slots["B"] = n_inv
+
+    env["handover"] = handover
     for s in slots_used:  # garbage everywhere but F
         slots[s] = O.f12_pow(f, rng.randrange(2, 1000)) if s != "F" else f
     exec(fc_src, dict(env))
