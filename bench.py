@@ -1106,11 +1106,15 @@ def main():
     # batches in flight run on unpadded lanes: the 12-lane pairing kernel with
     # its line kernels (bn256_sig12.hip); one batch at a time, the padded
     # 16-lane k_verify_sig (hg_api.cpp: sig12_for)
-    sig_kernel = (r"k_verify_sig12<false>|k_sig_(lines|scalars)" if inflight > 1
-                  else r"k_verify_sig<4, true(, true)?>")
+    # (the 12-lane pairing runs split around its norm inversion since r06:
+    # k_sig12_miller, k_sig12_ninv, k_sig12_fe; k_verify_sig12 with
+    # HG_SIG12_SPLIT=0)
+    sig_kernel = (r"(k_verify_sig12|k_sig12_miller|k_sig12_fe)<false>|k_sig12_ninv|k_sig_(lines|scalars)"
+                  if inflight > 1 else r"k_verify_sig<4, true(, true)?>")
     roof = roofline(impl_fpmul, agg_ms,
                     (f"the GT submission, {inflight} batches in flight (timed region per step): k_agg_prologue, "
-                     "k_sig_scalars + k_sig_lines + k_verify_sig12 (12-lane teams)" if inflight > 1
+                     "k_sig_scalars + k_sig_lines + k_sig12_miller + k_sig12_ninv + k_sig12_fe (12-lane teams)"
+                     if inflight > 1
                      else "the GT submission: k_agg_prologue, k_verify_sig") + " beside the GT fold (k_gt_plan, "
                     "k_gt_chunks, k_gt_combine), k_gt_compare_bits",
                     r"k_agg_prologue|k_gt_(plan<16>|chunks|combine|compare_bits)|" + sig_kernel,
@@ -1155,8 +1159,9 @@ def main():
                            f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (one pairing "
                            "+ final exponentiation, oracle op count); kernel alone (fold not beside it)",
                            rocprof_pattern=r"k_verify_sig<4, true(, (true|false))?>")
-    # the headline's pairing kernel alone: k_sig_scalars + k_sig_lines +
-    # k_verify_sig12 on one stream, HIP events around 5 launches. Its padded
+    # the headline's pairing kernels alone: k_sig_scalars + k_sig_lines +
+    # k_sig12_miller + k_sig12_ninv + k_sig12_fe on one stream, HIP events
+    # around 5 launches. Its padded
     # form (hg_sig_pairing_device kernel 2): one batch alone occupies 820 of
     # the 1024 SIMDs with one wave each — the unpadded form alone would let
     # the dispatcher stack two waves on some SIMDs and leave others empty —
@@ -1175,11 +1180,13 @@ def main():
     torch.cuda.synchronize(dev)
     sig12_ms = ev[0].elapsed_time(ev[1]) / 5
     del d_fe
-    roof_sig12 = roofline(n * FPMUL_PER_SIG_PAIRING, sig12_ms, "k_sig_scalars + k_sig_lines + k_verify_sig12<true>",
-                          r"k_verify_sig12<true>|k_sig_(lines|scalars)",
+    sig12_pad = r"(k_verify_sig12|k_sig12_miller|k_sig12_fe)<true>|k_sig12_ninv|k_sig_(lines|scalars)"
+    roof_sig12 = roofline(n * FPMUL_PER_SIG_PAIRING, sig12_ms,
+                          "k_sig_scalars + k_sig_lines + k_sig12_miller<true> + k_sig12_ninv + k_sig12_fe<true>",
+                          sig12_pad,
                           f"{FPMUL_PER_SIG_PAIRING} Fp-mul x {MADS_PER_FPMUL} u32 mads per check (the line "
                           "evaluations included); one launch alone, one wave per SIMD",
-                          rocprof_pattern=r"k_verify_sig12<true>|k_sig_(lines|scalars)")
+                          rocprof_pattern=sig12_pad)
     roof_fold = roofline(head.terms * FPMUL_PER_GT_MUL, ph_seq["fold"], "k_gt_plan + k_gt_chunks + k_gt_combine",
                          r"k_gt_(plan<16>|chunks|combine)",
                          f"{head.terms} window-table terms x {FPMUL_PER_GT_MUL} Fp-mul (one Fp12 product each); "

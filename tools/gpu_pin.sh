@@ -18,7 +18,7 @@ export TMPDIR=/tmp
 D="bench.py --steps 20 --warmup 5"
 H="bench.py --steps 20 --warmup 5 --no-cpu --no-extra"
 S="bench.py --steps 5 --warmup 1 --no-cpu --no-service --pipeline 1"
-K="k_verify_sig|k_sig_|k_gt_|k_agg_"
+K="k_verify_sig|k_sig_|k_sig12|k_gt_|k_agg_"
 timeout -k 10 600 python3 $D > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run -- python3 $D > $OUT/bench_traced.json 2> $OUT/traced.err &&
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $OUT/fetch -o run -- python3 $H > $OUT/fetch.log 2>&1 &&
