@@ -671,11 +671,17 @@ int hg_service_create(hg_ctx* ctx, const char* name, const hg_service_config* cf
   if (rc) return rc;
   GpuExec* g = new GpuExec(ctx);
   const size_t max_words = (size_t)s->cfg.max_batch * s->v.h->slot_words;
+  // HG_SERVICE_PAD=0: unpadded lanes (the 12-lane split pairing, two waves of
+  // different batches per SIMD) instead of the padded 16-lane kernel (one wave
+  // per SIMD: the latency form); an A/B knob (tools/gpu_service_pad.sh)
+  const char* pe = getenv("HG_SERVICE_PAD");
+  const bool pad = !pe || atoi(pe) != 0;
   for (uint32_t i = 0; i < s->cfg.lanes; i++) {
     hg_lane* l = nullptr;
     rc = hg_lane_create(ctx, s->cfg.max_batch, max_words, s->cfg.overlap, &l);
+    if (rc == HG_OK && !pad) rc = hg_lane_set_pairing_padding(l, 0);
+    if (l) g->ln.push_back(l);
     if (rc) break;
-    g->ln.push_back(l);
   }
   if (rc) {
     delete g;

@@ -59,6 +59,7 @@ int hg_lane_query(hg_lane*) { return -1; }
 int hg_lane_wait(hg_lane*) { return HG_ERR_DEVICE; }
 const int32_t* hg_lane_codes(hg_lane*) { return nullptr; }
 int hg_lane_set_latency_form(hg_lane*, int) { return HG_ERR_DEVICE; }
+int hg_lane_set_pairing_padding(hg_lane*, int) { return HG_ERR_DEVICE; }
 }
 
 using namespace hgshm;
