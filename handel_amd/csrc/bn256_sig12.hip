@@ -366,7 +366,8 @@ bool sig12_for(bool pad, size_t n) {
   return n <= (size_t)kSig12MaxN && (mode == 1 || (mode == -1 && !pad));
 }
 
-// the split form (k_sig12_miller, k_sig12_ninv, k_sig12_fe) unless HG_SIG12_SPLIT=0
+// the split form (k_sig12_miller, k_sig12_ninv, k_sig12_fe) for unpadded
+// launches unless HG_SIG12_SPLIT=0
 static bool sig12_split() {
   static const bool on = [] {
     const char* e = getenv("HG_SIG12_SPLIT");
@@ -397,15 +398,17 @@ void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef
   k_sig_scalars<<<(n + kLineBlock - 1) / kLineBlock, kLineBlock, 0, s>>>(sigs, flavor, n, sc);
   k_sig_lines<<<dim3((4 * n + kLineBlock - 1) / kLineBlock, kNumLines), kLineBlock, 0, s>>>(sc, n, tab, ev);
   const int blocks = (n + kTeams12 - 1) / kTeams12;
-  if (sig12_split()) {
+  // the split form for unpadded launches only (batches in flight share the
+  // SIMDs, so the inversion kernel's latency hides behind other batches'
+  // waves); a padded launch runs alone at one wave per SIMD, where the single
+  // kernel is faster (0.947 vs 0.964 ms per 4096, profiles/r06b_sig12_split_ab.json)
+  if (sig12_split() && !pad) {
     SigHand* hand = (SigHand*)(base + sig12_hand_offset(n));
     Fp* nrm = (Fp*)(base + sig12_norm_offset(n));
     Fp* ninv = (Fp*)(base + sig12_ninv_offset(n));
-    if (pad) k_sig12_miller<true><<<blocks, 64, 0, s>>>(ev, n, fe, hand, nrm);
-    else k_sig12_miller<false><<<blocks, 64, 0, s>>>(ev, n, fe, hand, nrm);
+    k_sig12_miller<false><<<blocks, 64, 0, s>>>(ev, n, fe, hand, nrm);
     k_sig12_ninv<<<(n + kInvBlock - 1) / kInvBlock, kInvBlock, 0, s>>>(nrm, n, ninv);
-    if (pad) k_sig12_fe<true><<<blocks, 64, 0, s>>>(n, fe, park, hand, ninv);
-    else k_sig12_fe<false><<<blocks, 64, 0, s>>>(n, fe, park, hand, ninv);
+    k_sig12_fe<false><<<blocks, 64, 0, s>>>(n, fe, park, hand, ninv);
     return;
   }
   if (pad) k_verify_sig12<true><<<blocks, 64, 0, s>>>(ev, n, fe, park);

@@ -223,9 +223,10 @@ np.save(sys.argv[1], np.concatenate(out))
 
 def test_split_sig12_matches_the_monolithic_kernel(tmp_path):
     """The 12-lane pairing in three kernels (k_sig12_miller, the batched norm
-    inversion k_sig12_ninv, k_sig12_fe: the default) and in one
-    (k_verify_sig12, HG_SIG12_SPLIT=0) write byte-identical FE values, padded
-    and unpadded, both flavors, ragged n (a 1029-check batch spans five
+    inversion k_sig12_ninv, k_sig12_fe: the default for unpadded launches) and
+    in one (k_verify_sig12: padded launches, and every launch with
+    HG_SIG12_SPLIT=0) write byte-identical FE values, both kernels 2 and 3 in
+    both settings, both flavors, ragged n (a 1029-check batch spans five
     inversion blocks, the last one partly empty), with a point at infinity in
     the batch. Each form runs in a child process (the switch is read once per
     process)."""
