@@ -269,7 +269,8 @@ int hg_debug_fp12(hg_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_
  * 64-byte signature marshals at d_sigs (context flavor), computed by kernel
  * 0: k_verify_sig padded (one wave per SIMD), 1: k_verify_sig unpadded,
  * 2: k_sig_scalars + k_sig_lines + k_verify_sig12 padded, 3: the same
- * unpadded (what a lane in flight runs), 4: k_verify_sig_split<2> (two
+ * unpadded (what a lane in flight runs: since r06 split into k_sig12_miller,
+ * k_sig12_ninv, k_sig12_fe unless HG_SIG12_SPLIT=0), 4: k_verify_sig_split<2> (two
  * waves per check: the padded latency form for n <= 2048). Enqueued on `stream` (NULL: the
  * context's), ordered like every submission of the context. Replaces no
  * reference interface: the product paths choose the kernel themselves. */
