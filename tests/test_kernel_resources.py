@@ -36,10 +36,10 @@ def _one(res, part):
 
 HOT = {
     # mangled-name fragment: (LDS bytes, VGPR rule)
-    "k_verify_sig12ILb0E": (18800, "two_per_simd"),   # the headline's unpadded 12-lane kernel
-    "k_verify_sig12ILb1E": (18800, "padded"),
-    "k_sig12_millerILb0E": (18800, "two_per_simd"),   # the split form's two halves (the default)
-    "k_sig12_feILb0E": (18800, "two_per_simd"),
+    "k_verify_sig12ILb0E": (18400, "two_per_simd"),   # the headline's unpadded 12-lane kernel
+    "k_verify_sig12ILb1E": (18400, "padded"),
+    "k_sig12_millerILb0E": (18400, "two_per_simd"),   # the split form's two halves (the default)
+    "k_sig12_feILb0E": (18400, "two_per_simd"),
     "k_sig12_ninv": (20480, None),
     "k_verify_sigILi4ELb1ELb1E": (18880, "padded"),   # k_verify_sig<4, true, true>: sequential / latency
     "k_verify_sig_splitILi2E": (30144, "padded"),     # the two-wave latency form

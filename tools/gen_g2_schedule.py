@@ -383,6 +383,55 @@ def prog_cyc_sqr_x():
     return [lanes]
 
 
+def prog_cyc_sqr_x_shared():
+    """CYC_SQR_X's forms rewritten so that the lanes share their operand
+    combinations (r06, the 12-lane teams: 24 pre-pass values instead of 31,
+    two per lane on lanes 0..11 instead of three). The b-part of a squared
+    group's two lanes,
+        3(a^2 + xi b^2).x  b-part:  3 by^2 + 18 bx by - 3 bx^2 = bx V1 + by V2
+        3(a^2 + xi b^2).y  b-part:  9 by^2 -  6 bx by - 9 bx^2 = by V1 + (-bx) V2
+    with V1 = 9 by - 3 bx, V2 = 9 bx + 3 by, uses three values (V1, V2, -bx)
+    where CYC_SQR_X uses five (18 bx, 3(by + bx), by - bx, -6 bx,
+    9(by + bx)); the xi lanes of group 2 share -bx. Still at most three
+    products per lane, plus -2c / +2c as a linear term."""
+    def e(name, c):
+        return comp(name, c)
+
+    lanes = []
+    groups = {0: ("A0", "A3"), 1: ("A1", "A4"), 2: ("A2", "A5")}
+    kinds = {0: (0, "sq"), 3: (0, "ab"), 2: (1, "sq"), 5: (1, "ab"), 4: (2, "sq"), 1: (2, "xi")}
+    for k in range(6):
+        g, kind = kinds[k]
+        a, b = groups[g]
+        ax, ay, bx, by = e(a, "x"), e(a, "y"), e(b, "x"), e(b, "y")
+        v1 = [(by, 9), (bx, -3)]
+        v2 = [(bx, 9), (by, 3)]
+        nbx = [(bx, -1)]
+        for c in "xy":
+            if kind == "sq":
+                if c == "x":
+                    slots = [([(ax, 6)], [(ay, 1)]), ([(bx, 1)], v1), ([(by, 1)], v2)]
+                else:
+                    slots = [([(ay, 3), (ax, 3)], [(ay, 1), (ax, -1)]), ([(by, 1)], v1), (nbx, v2)]
+                lin = [(e(f"A{k}", c), -2)]
+            elif kind == "ab":
+                if c == "x":
+                    slots = [([(ax, 6)], [(by, 1)]), ([(ay, 6)], [(bx, 1)])]
+                else:
+                    slots = [([(ay, 6)], [(by, 1)]), ([(ax, -6)], [(bx, 1)])]
+                lin = [(e(f"A{k}", c), 2)]
+            else:
+                u = [(ax, 18), (ay, 6)]
+                v = [(ay, 18), (ax, -6)]
+                if c == "x":
+                    slots = [(u, [(by, 1)]), (v, [(bx, 1)])]
+                else:
+                    slots = [(v, [(by, 1)]), (u, nbx)]
+                lin = [(e(f"A{k}", c), 2)]
+            lanes.append(Lane(comp(f"D{k}", c), slots + [(lin, one())]))
+    return [lanes]
+
+
 def prog_sqr12():
     """f^2 in Fp2[w]/(w^6 - xi): c_k = sum_{i<=j, i+j = k mod 6} (2 - [i==j]) a_i a_j xi^[i+j>=6]."""
     def xi_prod(i, j, c, mult):
@@ -526,7 +575,7 @@ PROGRAMS["MUL12F"] = prog_mul12()
 PROGRAMS["SQR12_12"] = prog_sqr12()
 PROGRAMS["LINE_FIX_12"] = prog_line_n("FB", "FC")
 PROGRAMS["MUL12_12"] = prog_mul12()
-PROGRAMS["CYC_SQR_X_12"] = prog_cyc_sqr_x()
+PROGRAMS["CYC_SQR_X_12"] = prog_cyc_sqr_x_shared()  # r06: 24 pre-pass values (two per lane)
 # programs also emitted in the single-phase table format (bn256_g2sched.h)
 LEGACY = ("DBL", "ADD_POS", "ADD_NEG", "ADD_F1", "ADD_F2", "CYC_SQR", "SQR12")
 
