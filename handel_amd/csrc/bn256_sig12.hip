@@ -22,10 +22,11 @@
 // 340 threads: the whole GPU, a few microseconds per batch).
 //
 // Team region (layout T, tools/gen_g2_schedule.py): five Fp12 slots and the
-// register file, 94 elements — the final exponentiation parks two of its
-// seven live values in HBM (bn256_sigfe.h team_final_exp_fc_t) — so a wave of
-// five teams takes 18.8 KB of LDS and a CU holds eight pairing waves (two
-// per SIMD: the unpadded kernel's 247 VGPRs allow it) beside a fold
+// register file, 92 elements (kSigTTeamElems; 94 before the shared-operand
+// squaring of r06) — the final exponentiation parks two of its seven live
+// values in HBM (bn256_sigfe.h team_final_exp_fc_t) — so a wave of five teams
+// takes 18.4 KB of LDS and a CU holds eight pairing waves (two per SIMD: the
+// unpadded kernels' 193-212 VGPRs allow it) beside a fold
 // workgroup.
 //
 // Values are identical to k_verify_sig's (the same Montgomery products in the
@@ -152,7 +153,7 @@ HG_DEV void team_miller_sig12(const Team& T, uint32_t* F, const Fp* ev, int n, i
 }
 
 // fe[r] = FE(Miller(G2Base at -sig_r)) on layout T (kSigTTeamElems elements
-// per team: 18.8 KB of LDS per wave), five teams per wave. The final
+// per team: 18.4 KB of LDS per wave), five teams per wave. The final
 // exponentiation parks two values per check in HBM: fe[r] itself (the result
 // overwrites it) and park[r]. kPad: one pairing wave per SIMD (as
 // k_verify_sig's default); unpadded, two batches' waves share a SIMD.

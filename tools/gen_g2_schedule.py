@@ -1260,7 +1260,8 @@ SIG_INSTANCES = sorted(set(
 # HBM while the exponentiations by u run (bn256_sigfe.h team_final_exp_fc_t),
 # so five slots are live at most — then the register file (ZERO, ONE; the
 # Miller loop's FB, FC; the final exponentiation's pre-pass scratch from
-# register 2 on). 94 elements: five 12-lane teams take 18.8 KB of LDS per
+# register 2 on). 92 elements (94 before the r06 shared-operand squaring):
+# five 12-lane teams take 18.4 KB of LDS per
 # wave, so a CU holds eight pairing waves (two per SIMD) and a fold workgroup.
 SIG_T_SLOTS = SLOTS[:5]
 SIG_T_F_BASE = 12 * len(SIG_T_SLOTS)
