@@ -72,6 +72,7 @@ SIGNATURES = {
     "hg_set_aggregate_level": (_I, [_P, _I]),
     "hg_set_table_budget": (_I, [_P, _SZ]),
     "hg_set_fold_overlap": (_I, [_P, _I]),
+    "hg_set_verify_split": (_I, [_P, _I]),
     "hg_registry_non_g2": (_SZ, [_P]),
     "hg_set_message": (_I, [_P, _P, _SZ]),
     "hg_verify_batch": (_I, [_P, _P, _P, _SZ, _P]),

@@ -93,6 +93,11 @@ void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef
 // indexes 4 n threads in int) is never taken
 constexpr int kSig12MaxN = 1 << 28;
 bool sig12_for(bool pad, size_t n = 0);
+// the split chain's final exponentiation (k_sig12_norm, k_sig12_ninv,
+// k_sig12_fe) of n Miller values in fe, in place: config 2's second half
+// (launch_verify_split); ws: fe12_ws_bytes(n) bytes
+size_t fe12_ws_bytes(int n);
+void launch_fe12(Gt* fe, int n, uint8_t* ws, hipStream_t s);
 void launch_gt_compare(const Gt* fe, const Gt* y, int n, int32_t* codes, hipStream_t s);
 // the same, and the verdict bitset (ceil(n / 8) bytes, hg_pack_verdicts_device's layout)
 void launch_gt_compare_bits(const Gt* fe, const Gt* y, int n, int32_t* codes, uint8_t* bits, hipStream_t s);

@@ -45,6 +45,12 @@ void launch_g1_mul(const PointG1* base, const uint8_t* scalars, int n, PointG1* 
 void launch_hash_point(const uint32_t* k, PointG1* out, hipStream_t s);
 void launch_g2_lines(LineCoef* tab, hipStream_t s);
 void launch_verify(const CheckIn* in, int n, const LineCoef* tab, const PointG1* h, int32_t* codes, hipStream_t s);
+// the same checks in two halves (k_verify_ml on a compact team region, then
+// the 12-lane final exponentiation): the form for batches in flight; ws:
+// verify_split_ws_bytes(n) bytes
+size_t verify_split_ws_bytes(int n);
+void launch_verify_split(const CheckIn* in, int n, const LineCoef* tab, const PointG1* h, int32_t* codes,
+                         uint8_t* ws, hipStream_t s);
 void launch_pair(const PointG1* g1s, const PointG2* g2s, int n, const LineCoef* tab, uint8_t* gt, hipStream_t s);
 // blocks/block_base: the aligned block sums of the registry (hg_registry_load);
 // level k block j at blocks[block_base[k] + j] for 1 <= k <= levels

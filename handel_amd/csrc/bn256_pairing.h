@@ -262,35 +262,58 @@ HG_DEV void unit_line_pk(const Team& T, uint32_t* F, const CheckCtx& C) {
 // is MDBL_1 (f^2 beside the doubling's first round), MDBL_2 (f * G2Base line
 // beside its second round) and the pk line; an addition step is PADD_*_1,
 // MADD_*_2 (f * G2Base line beside the second round), PADD_*_3, pk line.
-using IMdbl1 = XInst<XP_MDBL_1, S_F, S_F>;
-using IMdbl2 = XInst<XP_MDBL_2, S_F, S_F>;
 template <int P1, int P2, int P3>
 struct AddStep {
   using I1 = XInst<P1>;
   using I2 = XInst<P2, S_F, S_F>;
   using I3 = XInst<P3>;
 };
-using AddPos = AddStep<XP_PADD_POS_1, XP_MADD_POS_2, XP_PADD_POS_3>;
-using AddNeg = AddStep<XP_PADD_NEG_1, XP_MADD_NEG_2, XP_PADD_NEG_3>;
-using AddF1 = AddStep<XP_PADD_F1_1, XP_MADD_F1_2, XP_PADD_F1_3>;
-using AddF2 = AddStep<XP_PADD_F2_1, XP_MADD_F2_2, XP_PADD_F2_3>;
+// ... bound to a team region: the full layout (MillerFull: k_verify,
+// k_gt_keys, k_pair) or layout V (MillerV: k_verify_ml, the Miller loop alone)
+struct MillerFull {
+  using Mdbl1 = XInst<XP_MDBL_1, S_F, S_F>;
+  using Mdbl2 = XInst<XP_MDBL_2, S_F, S_F>;
+  using Pdbl1 = XInst<XP_PDBL_1>;
+  using LinePk = XInst<XP_LINE_PK, S_F, S_F>;
+  using AddPos = AddStep<XP_PADD_POS_1, XP_MADD_POS_2, XP_PADD_POS_3>;
+  using AddNeg = AddStep<XP_PADD_NEG_1, XP_MADD_NEG_2, XP_PADD_NEG_3>;
+  using AddF1 = AddStep<XP_PADD_F1_1, XP_MADD_F1_2, XP_PADD_F1_3>;
+  using AddF2 = AddStep<XP_PADD_F2_1, XP_MADD_F2_2, XP_PADD_F2_3>;
+};
+struct MillerV {
+  using Mdbl1 = XInst<XP_MDBL_1_V, S_F, S_F>;
+  using Mdbl2 = XInst<XP_MDBL_2_V, S_F, S_F>;
+  using Pdbl1 = XInst<XP_PDBL_1_V>;
+  using LinePk = XInst<XP_LINE_PK_V, S_F, S_F>;
+  using AddPos = AddStep<XP_PADD_POS_1_V, XP_MADD_POS_2_V, XP_PADD_POS_3_V>;
+  using AddNeg = AddStep<XP_PADD_NEG_1_V, XP_MADD_NEG_2_V, XP_PADD_NEG_3_V>;
+  using AddF1 = AddStep<XP_PADD_F1_1_V, XP_MADD_F1_2_V, XP_PADD_F1_3_V>;
+  using AddF2 = AddStep<XP_PADD_F2_1_V, XP_MADD_F2_2_V, XP_PADD_F2_3_V>;
+};
 
-template <class A>
+template <class L, class A>
 HG_DEV void add_step(const Team& T, uint32_t* F, const CheckCtx& C, XStream& S, XHint next) {
   A::I1::run(T, S, xh<typename A::I2>());
   A::I2::run(T, S, xh<typename A::I3>());
-  A::I3::run(T, S, xh<ILinePk<S_F, S_F>>());
+  A::I3::run(T, S, xh<typename L::LinePk>());
   unit_line_pk(T, F, C);
-  x_line_pk<S_F, S_F>(T, S, next);
+  L::LinePk::run(T, S, next);
 }
 
 // f = Miller(pk at H) * Miller(G2Base at -sig) (x/crypto optate.go miller, with
 // the two loops sharing their squarings); the G2 steps run as team programs.
 // after: the program that runs after the loop.
+template <class L = MillerFull>
 HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, const LineCoef* tab, bool has_fixed,
                               XStream& S, XHint after) {
+  using IMdbl1 = typename L::Mdbl1;
+  using IMdbl2 = typename L::Mdbl2;
+  using AddPos = typename L::AddPos;
+  using AddNeg = typename L::AddNeg;
+  using AddF1 = typename L::AddF1;
+  using AddF2 = typename L::AddF2;
   const int8_t naf[kNafLen] = HG_NAF;
-  constexpr XHint kLinePk = xh<ILinePk<S_F, S_F>>();
+  constexpr XHint kLinePk = xh<typename L::LinePk>();
   t12_set_one(T, S_F);
   g2_regs_init(T, F, C, has_fixed);
   Fp held;
@@ -301,28 +324,28 @@ HG_DEV void team_miller_check(const Team& T, uint32_t* F, const CheckCtx& C, con
   for (int i = kNafLen - 1; i > 0; i--) {
     load_fixed_line(T, F, held, tab, ++s);
     DIAG_ADD(0);
-    if (i == kNafLen - 1) XInst<XP_PDBL_1>::run(T, S, xh<IMdbl2>());  // f = 1: no squaring
+    if (i == kNafLen - 1) L::Pdbl1::run(T, S, xh<IMdbl2>());  // f = 1: no squaring
     else IMdbl1::run(T, S, xh<IMdbl2>());
     DIAG_ADD(1);
     IMdbl2::run(T, S, kLinePk);
     unit_line_pk(T, F, C);
     DIAG_ADD(2);
     const int d = naf[i - 1];
-    const XHint step = i > 1 ? xh<IMdbl1>() : xh<AddF1::I1>();  // after this digit
-    x_line_pk<S_F, S_F>(T, S, d > 0 ? xh<AddPos::I1>() : d < 0 ? xh<AddNeg::I1>() : step);
+    const XHint step = i > 1 ? xh<IMdbl1>() : xh<typename AddF1::I1>();  // after this digit
+    L::LinePk::run(T, S, d > 0 ? xh<typename AddPos::I1>() : d < 0 ? xh<typename AddNeg::I1>() : step);
     DIAG_ADD(3);
     if (d != 0) {
       load_fixed_line(T, F, held, tab, ++s);
       DIAG_ADD(0);
-      if (d > 0) add_step<AddPos>(T, F, C, S, step);
-      else add_step<AddNeg>(T, F, C, S, step);
+      if (d > 0) add_step<L, AddPos>(T, F, C, S, step);
+      else add_step<L, AddNeg>(T, F, C, S, step);
       DIAG_ADD(4);
     }
   }
   load_fixed_line(T, F, held, tab, ++s);
-  add_step<AddF1>(T, F, C, S, xh<AddF2::I1>());
+  add_step<L, AddF1>(T, F, C, S, xh<typename AddF2::I1>());
   load_fixed_line(T, F, held, tab, ++s);
-  add_step<AddF2>(T, F, C, S, after);
+  add_step<L, AddF2>(T, F, C, S, after);
 }
 
 HG_DEV uint32_t* team_regs(const Team& T) { return T.base + kSlots * kFp12Words; }

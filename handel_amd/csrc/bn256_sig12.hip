@@ -210,6 +210,22 @@ struct SigHand {
   Fp v[8];  // t0, t1, t2, d (x, y each)
 };
 
+// lane tl < 8 stores term value tl, lane 8 the norm (team-uniform values)
+HG_DEV void sig12_store_terms(const Team& T, bool valid, const NormTerms& o, const Fp& nr, SigHand* hand, Fp* nrm) {
+  if (valid && T.tl < 9) {
+    Fp2 pick;  // (selects on values, not on member references: no scratch)
+    f2_sel(pick, T.tl < 6, o.t2, o.d);
+    f2_sel(pick, T.tl < 4, o.t1, pick);
+    f2_sel(pick, T.tl < 2, o.t0, pick);
+    Fp w;
+    fp_sel(w, (T.tl & 1) == 0, pick.x, pick.y);
+    fp_sel(w, T.tl == 8, nr, w);
+    uint2* dst = (uint2*)__builtin_assume_aligned(T.tl == 8 ? nrm->l : hand->v[T.tl].l, 8);
+#pragma unroll
+    for (int i = 0; i < 5; i++) dst[i] = make_uint2(w.l[2 * i], w.l[2 * i + 1]);
+  }
+}
+
 template <bool kPad>
 __global__ __launch_bounds__(64, kPad ? 1 : 2) void k_sig12_miller(const Fp* ev, int n, Gt* fe, SigHand* hand,
                                                                    Fp* nrm) {
@@ -235,19 +251,49 @@ __global__ __launch_bounds__(64, kPad ? 1 : 2) void k_sig12_miller(const Fp* ev,
 #pragma unroll
     for (int i = 0; i < 5; i++) dst[i] = make_uint2(v.l[2 * i], v.l[2 * i + 1]);
   }
-  // lane tl < 8 stores term value tl, lane 8 the norm (team-uniform values)
-  if (valid && T.tl < 9) {
-    Fp2 pick;  // (selects on values, not on member references: no scratch)
-    f2_sel(pick, T.tl < 6, o.t2, o.d);
-    f2_sel(pick, T.tl < 4, o.t1, pick);
-    f2_sel(pick, T.tl < 2, o.t0, pick);
-    Fp w;
-    fp_sel(w, (T.tl & 1) == 0, pick.x, pick.y);
-    fp_sel(w, T.tl == 8, nr, w);
-    uint2* dst = (uint2*)__builtin_assume_aligned(T.tl == 8 ? nrm[idx].l : hand[idx].v[T.tl].l, 8);
-#pragma unroll
-    for (int i = 0; i < 5; i++) dst[i] = make_uint2(w.l[2 * i], w.l[2 * i + 1]);
+  sig12_store_terms(T, valid, o, nr, hand + idx, nrm + idx);
+}
+
+// f = fe[c] into slot F of layout T, with the registers the programs read
+HG_DEV void sig12_load_f(const Team& T, uint32_t* F, const Gt* fe, int ci) {
+  if (T.tl == 0) {
+    Fp zero, one;
+    fp_zero(zero);
+    fp_one(one);
+    st_fp(F + R_ZERO * 10, zero);
+    st_fp(F + R_ONE * 10, one);
   }
+  const uint2* src = (const uint2*)__builtin_assume_aligned(fe[ci].w + 10 * T.e, 8);
+  uint32_t v[10];
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint2 x = src[i];
+    v[2 * i] = x.x;
+    v[2 * i + 1] = x.y;
+  }
+  if (T.active) st_fp_a8(slot(T, S_F) + T.e * 10, v);
+  team_sync();
+}
+
+// k_sig12_miller's second half for a Miller value computed elsewhere (config
+// 2's k_verify_ml, bn256_verify.hip): f = fe[c], the norm N = f conj(f)
+// (fe_t_norm), then t12_inv_norm up to d: the terms -> hand[c], n -> nrm[c]
+__global__ __launch_bounds__(64, 2) void k_sig12_norm(int n, const Gt* fe, SigHand* hand, Fp* nrm) {
+  constexpr int kWords = kSigTTeamElems * 10;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kTeams12 * kWords];
+  __builtin_amdgcn_s_setprio(3);
+  Team T = make_team12(lds, kWords);
+  uint32_t* F = T.base + kSigTRegBase * 10;
+  const int idx = blockIdx.x * kTeams12 + team12_index();
+  const bool valid = idx < n;
+  const int ci = valid ? idx : n - 1;
+  XStream S = x_stream();
+  sig12_load_f(T, F, fe, ci);
+  SigFE<SigProgs12>::fe_t_norm(T, S, xh_none());
+  NormTerms o;
+  Fp nr;
+  t12_inv_norm_terms(T, S_B, o, nr);
+  sig12_store_terms(T, valid, o, nr, hand + idx, nrm + idx);
 }
 
 // ninv[c] = nrm[c]^-1 (0 for 0: never the case for a Miller value, whose
@@ -311,26 +357,7 @@ __global__ __launch_bounds__(64, kPad ? 1 : 2) void k_sig12_fe(int n, Gt* fe, Gt
   const bool valid = idx < n;
   const int ci = valid ? idx : n - 1;
   XStream S = x_stream();
-  // the registers the programs read, f into slot F
-  if (T.tl == 0) {
-    Fp zero, one;
-    fp_zero(zero);
-    fp_one(one);
-    st_fp(F + R_ZERO * 10, zero);
-    st_fp(F + R_ONE * 10, one);
-  }
-  {
-    const uint2* src = (const uint2*)__builtin_assume_aligned(fe[ci].w + 10 * T.e, 8);
-    uint32_t v[10];
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const uint2 x = src[i];
-      v[2 * i] = x.x;
-      v[2 * i + 1] = x.y;
-    }
-    if (T.active) st_fp_a8(slot(T, S_F) + T.e * 10, v);
-  }
-  team_sync();
+  sig12_load_f(T, F, fe, ci);  // the registers the programs read, f into slot F
   t12_conj(T, S_D, S_F);
   NormTerms o;
   const SigHand& h = hand[ci];
@@ -388,6 +415,25 @@ static size_t sig12_hand_offset(int n) { return sig12_scalar_offset(n) + align25
 static size_t sig12_norm_offset(int n) { return sig12_hand_offset(n) + align256((size_t)n * sizeof(SigHand)); }
 static size_t sig12_ninv_offset(int n) { return sig12_norm_offset(n) + align256((size_t)n * sizeof(Fp)); }
 size_t sig12_lines_bytes(int n) { return sig12_ninv_offset(n) + (size_t)n * sizeof(Fp); }
+
+// The final exponentiation of n Miller values already in fe (config 2's
+// k_verify_ml), in place: k_sig12_norm, k_sig12_ninv, k_sig12_fe. ws:
+// fe12_ws_bytes(n) bytes (parking records, hand-over terms, norms, inverses).
+static size_t fe12_hand_offset(int n) { return align256((size_t)(n + 1 + 2 * kTeams12) * sizeof(Gt)); }
+static size_t fe12_norm_offset(int n) { return fe12_hand_offset(n) + align256((size_t)n * sizeof(SigHand)); }
+static size_t fe12_ninv_offset(int n) { return fe12_norm_offset(n) + align256((size_t)n * sizeof(Fp)); }
+size_t fe12_ws_bytes(int n) { return fe12_ninv_offset(n) + (size_t)n * sizeof(Fp); }
+void launch_fe12(Gt* fe, int n, uint8_t* ws, hipStream_t s) {
+  if (n <= 0 || n > kSig12MaxN) return;
+  Gt* park = (Gt*)ws;
+  SigHand* hand = (SigHand*)(ws + fe12_hand_offset(n));
+  Fp* nrm = (Fp*)(ws + fe12_norm_offset(n));
+  Fp* ninv = (Fp*)(ws + fe12_ninv_offset(n));
+  const int blocks = (n + kTeams12 - 1) / kTeams12;
+  k_sig12_norm<<<blocks, 64, 0, s>>>(n, fe, hand, nrm);
+  k_sig12_ninv<<<(n + kInvBlock - 1) / kInvBlock, kInvBlock, 0, s>>>(nrm, n, ninv);
+  k_sig12_fe<false><<<blocks, 64, 0, s>>>(n, fe, park, hand, ninv);
+}
 
 void launch_sig_pairing12(const uint8_t* sigs, int flavor, int n, const LineCoef* tab, Fp* ev, Gt* fe,
                           hipStream_t s, bool pad) {

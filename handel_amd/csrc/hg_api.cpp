@@ -166,7 +166,9 @@ struct Ws {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   DevBuf<Gt> gt_fe;
-  DevBuf<uint8_t> sig_lines;  // launch_sig_pairing12: the batch's lines evaluated at -sig
+  // launch_sig_pairing12: the batch's lines evaluated at -sig; launch_verify_split
+  // (config 2): the Miller values and the final exponentiation's records
+  DevBuf<uint8_t> sig_lines;
   void release() {
     pts2.release();
     pts1.release();
@@ -276,6 +278,7 @@ struct hg_ctx {
   // budget; hg_set_table_budget re-derives gt_cap from this)
   int oom_cap = 2;
   bool overlap = true;  // hg_set_fold_overlap; HG_GT_OVERLAP=0 gives new contexts false
+  bool verify_split = false;  // hg_set_verify_split; HG_VERIFY_SPLIT=1 gives new contexts true
   // submission order across streams: the event recorded after the last
   // submission and the stream it ran on (the workspaces above are shared)
   hipEvent_t last_ev = nullptr;
@@ -386,9 +389,15 @@ struct PhaseTimer {
   }
 };
 
-static void timed_verify(hg_ctx* c, const CheckIn* in, int n, int32_t* codes, hipStream_t s) {
+// config 2's split form (launch_verify_split: the Miller loop on a compact
+// team region, the 12-lane final exponentiation): hg_set_verify_split
+static bool verify_split_for(const hg_ctx* c, size_t n) { return c->verify_split && n <= (size_t)kSig12MaxN; }
+
+static void timed_verify(hg_ctx* c, const CheckIn* in, int n, int32_t* codes, hipStream_t s,
+                         uint8_t* split_ws = nullptr) {
   PhaseTimer t(c, HG_PHASE_VERIFY, s);
-  launch_verify(in, n, c->d_lines, c->d_h, codes, s);
+  if (split_ws) launch_verify_split(in, n, c->d_lines, c->d_h, codes, split_ws, s);
+  else launch_verify(in, n, c->d_lines, c->d_h, codes, s);
   t.stop();
 }
 
@@ -530,12 +539,14 @@ static int verify_batch_device_locked(hg_ctx* c, const uint8_t* d_pks, const uin
     return HG_ERR_ARG;
   }
   HG_CHECK(c, c->ws.checks.ensure(n));
+  const bool split = verify_split_for(c, n);
+  if (split) HG_CHECK(c, c->ws.sig_lines.ensure(verify_split_ws_bytes((int)n)));
   Submission sub(c, s);
   HG_CHECK(c, sub.start());
   PhaseTimer all(c, HG_PHASE_SUBMIT, s);
   launch_decode_checks(d_pks, d_sigs, (int)n, c->flavor, c->ws.checks.p, d_codes, s);
   if (c->hash_eof) k_fill_codes<<<nb(n), 256, 0, s>>>(d_codes, (int)n, HG_OK, HG_ERR_HASH_EOF);
-  else timed_verify(c, c->ws.checks.p, (int)n, d_codes, s);
+  else timed_verify(c, c->ws.checks.p, (int)n, d_codes, s, split ? c->ws.sig_lines.p : nullptr);
   all.stop();
   int rc = check_launch(c);
   if (rc) return rc;
@@ -1089,6 +1100,7 @@ int hg_create(int device, int flavor, hg_ctx** out) {
   c->flavor = flavor;
   c->pinned_level = gt_forced_level();
   c->overlap = gt_overlap();
+  c->verify_split = env_int("HG_VERIFY_SPLIT", 0, 0, 1) != 0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->d_lines, sizeof(LineCoef) * kNumLines);
@@ -1275,6 +1287,13 @@ int hg_set_fold_overlap(hg_ctx* c, int on) {
   if (!c) return HG_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->overlap = on != 0;
+  return HG_OK;
+}
+
+int hg_set_verify_split(hg_ctx* c, int on) {
+  if (!c) return HG_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->verify_split = on != 0;
   return HG_OK;
 }
 

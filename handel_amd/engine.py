@@ -109,6 +109,11 @@ class Engine:
         (hg_set_fold_overlap); same verdicts."""
         self._check(self.L.hg_set_fold_overlap(self.ctx, int(bool(on))), "hg_set_fold_overlap")
 
+    def set_verify_split(self, on: bool) -> None:
+        """Config 2's form (hg_set_verify_split): True = the split form for
+        batches in flight on several contexts; same verdicts."""
+        self._check(self.L.hg_set_verify_split(self.ctx, int(bool(on))), "hg_set_verify_split")
+
     def set_table_budget(self, nbytes: int) -> None:
         """Upper bound for this context's GT tables (hg_set_table_budget)."""
         self._check(self.L.hg_set_table_budget(self.ctx, int(nbytes)), "hg_set_table_budget")

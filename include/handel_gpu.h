@@ -191,6 +191,13 @@ int hg_set_aggregate_level(hg_ctx* ctx, int level);
  * (0). Same verdicts; the overlap hides the fold when one batch is in flight,
  * several contexts each with a batch in flight may prefer 0. */
 int hg_set_fold_overlap(hg_ctx* ctx, int on);
+/* Config 2 (hg_verify_batch*): the check's form. 0 (the default; HG_VERIFY_SPLIT
+ * gives new contexts its value): one kernel per batch, the faster form when a
+ * batch runs alone. 1: the split form — the Miller loop on a compact team
+ * region, then the 12-lane final exponentiation with batched inversions — for
+ * several contexts each keeping a batch in flight, whose waves then share the
+ * SIMDs. Same verdicts (PublicKey.VerifySignature, bn256/go/bn256.go:82-94). */
+int hg_set_verify_split(hg_ctx* ctx, int on);
 /* Upper bound in bytes for this context's GT tables (default: unlimited, the
  * device's free memory decides). Processes sharing one GPU (simul's P
  * processes x k instances, simul/node/main.go:63-131) give each context a

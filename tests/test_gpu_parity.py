@@ -345,3 +345,60 @@ def test_pack_verdicts_matches_codes(engine, n):
     want = np.packbits(np.concatenate([codes == 0, np.zeros((-n) % 8, bool)]), bitorder="little")
     assert np.array_equal(d_bits.cpu().numpy(), want)
     assert torch.equal(d_bits, pack_verdicts(d_codes))
+
+
+@pytest.mark.parametrize("flavor", ["go", "cf"])
+def test_verify_split_form_matches_oracle(flavor):
+    """Config 2's split form (hg_set_verify_split: k_verify_ml on the compact
+    team region, the 12-lane final exponentiation with batched inversions,
+    k_fe_verdicts): 4100 ragged checks plus the edge cases of
+    test_verify_batch_edge_cases (infinity pk and/or sig, off-curve points)
+    against the C restatement, and two contexts with a batch in flight each on
+    their own streams give the same codes as the one-kernel form."""
+    import torch
+
+    import bench
+    from handel_amd.engine import Engine
+
+    dev = torch.device("cuda:0")
+    n = 4100
+    one = Engine(device=0, flavor=flavor)
+    split = [Engine(device=0, flavor=flavor) for _ in range(2)]
+    try:
+        for e in [one] + split:
+            assert e.set_message(F.LIB_MESSAGE) == 0
+        for e in split:
+            e.set_verify_split(True)
+        pks, sigs, expect = bench.make_batch(one, n, seed=77)
+        # edge cases in the tail: infinity pk / sig, off-curve points
+        z128, z64 = bytes(128), bytes(64)
+        off_g1 = (1).to_bytes(32, "big") + (1).to_bytes(32, "big")
+        off_g2 = bytes(127) + b"\x01"
+        pks = pks + z128 + z128 + pks[:128] + off_g2 + pks[128:256]
+        sigs = sigs + z64 + sigs[:64] + z64 + sigs[64:128] + off_g1
+        m = n + 5
+        # the one-kernel form against the oracle on the batch (its edge cases:
+        # test_verify_batch_edge_cases, test_cf_signature_decode_edge_cases),
+        # the split form against the one-kernel form on everything
+        want = one.verify_batch(pks, sigs)
+        assert np.array_equal(want[:n], R.verify_batch(F.LIB_MESSAGE, pks[:128 * n], sigs[:64 * n], nthreads=16,
+                                                       flavor=0 if flavor == "go" else 1))
+        if flavor == "go":
+            assert np.array_equal(want, R.verify_batch(F.LIB_MESSAGE, pks, sigs, nthreads=16, flavor=0))
+        assert np.array_equal(split[0].verify_batch(pks, sigs), want)
+        # both split contexts in flight at once on their own streams
+        d_pks = torch.frombuffer(bytearray(pks), dtype=torch.uint8).to(dev)
+        d_sigs = torch.frombuffer(bytearray(sigs), dtype=torch.uint8).to(dev)
+        codes = [torch.full((m,), -1, dtype=torch.int32, device=dev) for _ in split]
+        streams = [torch.cuda.Stream(dev) for _ in split]
+        torch.cuda.synchronize(dev)
+        for rep in range(3):
+            for e, c, s in zip(split, codes, streams):
+                e.verify_batch_device(d_pks.data_ptr(), d_sigs.data_ptr(), m, c.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize(dev)
+        for c in codes:
+            assert np.array_equal(c.cpu().numpy(), want)
+        assert np.array_equal(want[:n], expect)
+    finally:
+        for e in [one] + split:
+            e.close()

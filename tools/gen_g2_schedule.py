@@ -1276,8 +1276,19 @@ SIG_T_INSTANCES = sorted(set(
                                  ("F", "A", "D"), ("F", "A", "F"), ("F", "C", "F"), ("D", "D", "C"), ("C", "C", "D")]]
     + [("CYC_SQR_X_12", b) for b in [("C", "F"), ("C", "C"), ("D", "C"), ("D", "D"), ("C", "D"), ("C", "B"),
                                      ("A", "A"), ("B", "A")]]))
+# k_verify_ml's team region (layout "V", bn256_verify.hip, r06): the
+# two-pairing Miller loop of config 2 alone — f in slot F, the pre-pass values
+# of its programs right after it (MDBL_1's 50 at most), then the whole runtime
+# register file — 128 elements, so a 4-team wave takes 20.5 KB of LDS and a
+# CU holds seven (k_verify's 212-element region: four). The final
+# exponentiation runs on the 12-lane split kernels (bn256_sig12.hip).
+V_SCRATCH = 50
+V_F_BASE = 12 + V_SCRATCH
+V_INSTANCES = ([("MDBL_1", ("F", "F")), ("MDBL_2", ("F", "F")), ("PDBL_1", ()), ("LINE_PK", ("F", "F"))]
+               + [(f"PADD_{v}_{i}", ()) for v in ("POS", "NEG", "F1", "F2") for i in (1, 3)]
+               + [(f"MADD_{v}_2", ("F", "F")) for v in ("POS", "NEG", "F1", "F2")])
 ALL_INSTANCES = ([(n, b, "") for n, b in INSTANCES] + [(n, b, "S") for n, b in SIG_INSTANCES]
-                 + [(n, b, "T") for n, b in SIG_T_INSTANCES])
+                 + [(n, b, "T") for n, b in SIG_T_INSTANCES] + [(n, b, "V") for n, b in V_INSTANCES])
 
 
 
@@ -1297,6 +1308,9 @@ def bind(xr, binding, ctx, layout=""):
     if layout == "T":
         assert ctx in SIG_T_SCR_BASE and all(b in SIG_T_SLOTS for b in binding), "layout T: slots F..D only"
         sbase, fbase, region_end = SIG_T_SCR_BASE[ctx], SIG_T_F_BASE, SIG_T_F_BASE + NREGS_RUNTIME
+    if layout == "V":
+        assert ctx == "ML" and all(b == "F" for b in binding), "layout V: the Miller loop on slot F"
+        sbase, fbase, region_end = 12, V_F_BASE, V_F_BASE + NREGS_RUNTIME
 
     def src(code):
         if code >= X_SCR:
@@ -1335,6 +1349,8 @@ def bind(xr, binding, ctx, layout=""):
             assert all(d == NONE or 12 <= d < SIG_F_BASE for d, _ in L["pre"]), "layout S: ML scratch"
         if layout == "T" and ctx == "ML":  # ... inside slots A..D
             assert all(d == NONE or 12 <= d < SIG_T_F_BASE for d, _ in L["pre"]), "layout T: ML scratch"
+        if layout == "V":  # ... between slot F and the registers
+            assert all(d == NONE or 12 <= d < V_F_BASE for d, _ in L["pre"]), "layout V: ML scratch"
     out = XRound(xr.nv, xr.nt, xr.np, xr.nl, lanes, xr.name, xr.np2, xr.nl2)
     out.kp, out.kl1, out.kl2 = xr.kp, xr.kl1, xr.kl2
     out.ks1, out.ks2 = xr.ks1, xr.ks2
@@ -1364,7 +1380,7 @@ def check_instances(X, seed=3):
     rng = random.Random(seed)
     for name, binding, layout in ALL_INSTANCES:
         ctx = X_PROGRAMS[name]
-        fb = SIG_F_BASE if layout == "S" else (SIG_T_F_BASE if layout == "T" else F_BASE_CTX[ctx])
+        fb = {"S": SIG_F_BASE, "T": SIG_T_F_BASE, "V": V_F_BASE}.get(layout, F_BASE_CTX[ctx])
         rounds = [bind(xr, binding, ctx, layout) for xr in X[name]]
         mem = [rng.randrange(P) for _ in range(F_BASE + NREGS)]
         mem[fb + REG["ZERO"]] = 0
@@ -1420,6 +1436,8 @@ def emit_x(X, path):
                 fold_end = max(fold_end, t)
     sig_names = sorted({n for n, _, lay in ALL_INSTANCES if lay == "S"}, key=list(X_PROGRAMS).index)
     sig_t_names = sorted({n for n, _, lay in ALL_INSTANCES if lay == "T"}, key=list(X_PROGRAMS).index)
+    v_names = sorted({n for n, _, lay in ALL_INSTANCES if lay == "V"}, key=list(X_PROGRAMS).index)
+    v_end = V_F_BASE + NREGS_RUNTIME
     lines = ["// Generated by tools/gen_g2_schedule.py — do not edit.",
              "// Two-phase team programs executed by bn256_xprog.h (encoding: see there),",
              "// one table per call-site instance (absolute team element indices).",
@@ -1427,7 +1445,8 @@ def emit_x(X, path):
              f"// HG_P2N: ({NEG_MULT}p)'' (the negation constant of pre-pass and linear terms)",
              "#define HG_P2N " + ", ".join("0x%08xu" % v for v in P2N),
              "enum XProg { " + ", ".join([f"XP_{n}" for n in X_PROGRAMS] + [f"XP_{n}_S" for n in sig_names]
-                                         + [f"XP_{n}_T" for n in sig_t_names]) + " };",
+                                         + [f"XP_{n}_T" for n in sig_t_names]
+                                         + [f"XP_{n}_V" for n in v_names]) + " };",
              f"static constexpr int kXFetchWords = {X_FETCH_WORDS};",
              f"static constexpr int kFoldRegBase = {FOLD_F_BASE};  // FOLD team region: ZERO, ONE here",
              f"static constexpr int kFoldTeamElems = {fold_end + fold_end % 2};  // elements the fold programs touch",
@@ -1435,6 +1454,8 @@ def emit_x(X, path):
              f"static constexpr int kSigTeamElems = {sig_end + sig_end % 2};  // k_verify_sig's team region (layout S)",
              f"static constexpr int kSigTRegBase = {SIG_T_F_BASE};  // k_verify_sig12's layout T: registers here",
              f"static constexpr int kSigTTeamElems = {sig_t_end + sig_t_end % 2};  // k_verify_sig12's team region",
+             f"static constexpr int kVRegBase = {V_F_BASE};  // k_verify_ml's layout V: registers here",
+             f"static constexpr int kVTeamElems = {v_end + v_end % 2};  // k_verify_ml's team region",
              "template <int PROG, int D = -1, int A = -1, int B = -1> struct XInst;"]
     words = []
     for name, binding, layout in ALL_INSTANCES:
