@@ -69,9 +69,9 @@ __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const L
 // ---------------------------------------------------------------- split form (r06)
 // The same check in two halves, for batches in flight: k_verify_ml runs the
 // Miller loop alone on layout V (tools/gen_g2_schedule.py: f, its programs'
-// 50 pre-pass values, the register file — 128 elements, 20.5 KB per 4-team
-// wave where k_verify's 212-element region takes 33.6 KB, so seven waves fit
-// a CU instead of four) and stores f; the final exponentiation runs on five
+// 50 pre-pass values, the register file — 128 elements, 20480 bytes per
+// 4-team wave where k_verify's 212-element region takes 33.6 KB, so a CU's
+// 160 KiB holds eight waves, two per SIMD, instead of four) and stores f; the final exponentiation runs on five
 // 12-lane teams per wave with the norm inversions batched (launch_fe12,
 // bn256_sig12.hip); k_fe_verdicts tests FE == 1. Values, and verdicts, are
 // k_verify's: the same programs in the same order, and the FE chain is

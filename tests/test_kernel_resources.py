@@ -42,7 +42,7 @@ HOT = {
     "k_sig12_feILb0E": (18400, "two_per_simd"),
     "k_sig12_ninv": (20480, None),
     "k_sig12_norm": (18400, "two_per_simd"),          # config 2's split form: the norm of a given f
-    "k_verify_mlILi4E": (20480, "two_per_simd"),      # ... and its Miller loop on layout V (seven waves per CU)
+    "k_verify_mlILi4E": (20480, "two_per_simd"),      # ... and its Miller loop on layout V (eight waves per CU)
     "k_verify_sigILi4ELb1ELb1E": (18880, "padded"),   # k_verify_sig<4, true, true>: sequential / latency
     "k_verify_sig_splitILi2E": (30144, "padded"),     # the two-wave latency form
     "k_gt_chunks": (12000, None),

@@ -1279,8 +1279,9 @@ SIG_T_INSTANCES = sorted(set(
 # k_verify_ml's team region (layout "V", bn256_verify.hip, r06): the
 # two-pairing Miller loop of config 2 alone — f in slot F, the pre-pass values
 # of its programs right after it (MDBL_1's 50 at most), then the whole runtime
-# register file — 128 elements, so a 4-team wave takes 20.5 KB of LDS and a
-# CU holds seven (k_verify's 212-element region: four). The final
+# register file — 128 elements, so a 4-team wave takes 20480 bytes of LDS and
+# a CU's 160 KiB holds eight, two per SIMD (k_verify's 212-element region:
+# four). The final
 # exponentiation runs on the 12-lane split kernels (bn256_sig12.hip).
 V_SCRATCH = 50
 V_F_BASE = 12 + V_SCRATCH
