@@ -219,6 +219,21 @@ func (e *Engine) SetTableBudget(bytes uint64) error {
 	return nil
 }
 
+// SetVerifySplit selects config 2's form for this engine: true runs
+// VerifyBatch as the split form (the Miller loop on a compact team region,
+// then the 12-lane final exponentiation), the faster one when several engines
+// each keep a batch in flight on one GPU; same verdicts (hg_set_verify_split).
+func (e *Engine) SetVerifySplit(on bool) error {
+	v := C.int(0)
+	if on {
+		v = 1
+	}
+	if rc := C.hg_set_verify_split(e.ctx, v); rc != C.HG_OK {
+		return e.fail(rc)
+	}
+	return nil
+}
+
 // RegistryNonG2 is the number of loaded registry keys on the twist but
 // outside G2 (accepted by x/crypto's Unmarshal); such a registry is checked
 // with the G2 point fold and two pairings (hg_registry_non_g2).
