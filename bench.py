@@ -1298,11 +1298,24 @@ def main():
 
         rdt = timer.run(rstep, args.steps, args.warmup)
         assert np.array_equal(rcodes.cpu().numpy(), rexpect), "registry single-signature verdicts"
+
+        class _RegSingles:  # the batch in lanes_rate's shape
+            d_reqs, d_words, d_sigs = d_rreqs, d_rwords, d_rsigs
+
+            def check(self, codes):
+                assert np.array_equal(codes.cpu().numpy(), rexpect), "registry single-signature verdicts (lanes)"
+        _RegSingles.n = n
+        reg_inflight = None
+        if inflight > 1:
+            ridt = lanes_rate(eng, _RegSingles(), inflight, timer, args.steps, args.warmup, dev)
+            reg_inflight = {"value": round(n * args.steps * world / ridt, 1), "unit": "verifications/s",
+                            "ms_per_step": round(ridt / args.steps * 1e3, 4), "batches_in_flight": inflight,
+                            "what": "the same batches in flight on the context's lanes, as the headline runs"}
         progress("single_registry")
         extra["single_registry"] = {
             "metric": "BN254 single-sig verifications/sec, registry keys (batch 4096)",
             "value": round(n * args.steps * world / rdt, 1), "unit": "verifications/s",
-            "ms_per_step": round(rdt / args.steps * 1e3, 4),
+            "ms_per_step": round(rdt / args.steps * 1e3, 4), "inflight": reg_inflight,
             "workload": f"{n} single signatures from random nodes of the {n_reg}-key registry (one-key aggregate "
                         "requests: the GT path), lib.Message, 1/8 tampered"}
         # VerifyMultiSignature shape: every request spans the whole registry
