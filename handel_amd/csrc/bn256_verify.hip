@@ -16,17 +16,8 @@ __device__ uint64_t g_diag[4096 * 16];
 #endif
 
 
-// TEAMS checks per workgroup of 16 * TEAMS lanes (one wave; LDS sized to TEAMS)
-template <int TEAMS>
-__global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const LineCoef* tab,
-                                               const PointG1* hpt, int32_t* codes) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
-  Team T = make_team(lds, kTeamWords);
-  uint32_t* F = team_regs(T);
-  int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
-  bool valid = idx < n;
-  int ci = valid ? idx : n - 1;
-  const CheckIn& I = in[ci];
+// the Miller loop's per-check inputs (pk and sig decoded by k_decode_checks)
+HG_DEV CheckCtx check_ctx(const CheckIn& I, const PointG1* hpt) {
   CheckCtx C;
   C.qx = I.pk.x;
   C.qy = I.pk.y;
@@ -41,6 +32,21 @@ __global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const L
     C.qx = gx;
     C.qy = gy;
   }
+  return C;
+}
+
+// TEAMS checks per workgroup of 16 * TEAMS lanes (one wave; LDS sized to TEAMS)
+template <int TEAMS>
+__global__ __launch_bounds__(64) void k_verify(const CheckIn* in, int n, const LineCoef* tab,
+                                               const PointG1* hpt, int32_t* codes) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[TEAMS * kTeamWords];
+  Team T = make_team(lds, kTeamWords);
+  uint32_t* F = team_regs(T);
+  int idx = blockIdx.x * TEAMS + (threadIdx.x >> 4);
+  bool valid = idx < n;
+  int ci = valid ? idx : n - 1;
+  const CheckIn& I = in[ci];
+  const CheckCtx C = check_ctx(I, hpt);
 #ifdef HG_DIAG
   if (threadIdx.x < 16) hg_diag_acc[threadIdx.x] = 0;
   __syncthreads();
@@ -87,20 +93,7 @@ __global__ __launch_bounds__(64) void k_verify_ml(const CheckIn* in, int n, cons
   const bool valid = idx < n;
   const int ci = valid ? idx : n - 1;
   const CheckIn& I = in[ci];
-  CheckCtx C;
-  C.qx = I.pk.x;
-  C.qy = I.pk.y;
-  C.hx = hpt->x;
-  C.hy = hpt->y;
-  C.sx = I.sig.x;
-  C.sy = I.sig.y;
-  C.use_q = I.pk.inf == 0;
-  C.use_s = I.sig.inf == 0;
-  if (!C.use_q) {  // keep the (unused) doubling chain well-defined
-    const Fp2 gx = HG_G2X, gy = HG_G2Y;
-    C.qx = gx;
-    C.qy = gy;
-  }
+  const CheckCtx C = check_ctx(I, hpt);
   XStream S = x_stream();
   team_miller_check<MillerV>(T, F, C, tab, true, S, xh_none());
   Fp v;
