@@ -74,3 +74,5 @@ def test_null_handles_are_refused_without_gpu():
     assert L.hg_lane_set_latency_form(None, 2048) == _lib.HG_ERR_ARG
     assert L.hg_lane_set_pairing_padding(None, 1) == _lib.HG_ERR_ARG
     assert L.hg_sig_pairing_device(None, None, 0, None, 0, None) == _lib.HG_ERR_ARG
+    assert L.hg_set_verify_split(None, 1) == _lib.HG_ERR_ARG
+    assert L.hg_set_fold_overlap(None, 1) == _lib.HG_ERR_ARG
