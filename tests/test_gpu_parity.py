@@ -402,3 +402,25 @@ def test_verify_split_form_matches_oracle(flavor):
     finally:
         for e in [one] + split:
             e.close()
+
+
+def test_verify_split_form_small_batches(engine):
+    """The split form on batches smaller than one workgroup of either half
+    (1 and 7 checks: one partly filled 4-team Miller wave, one partly filled
+    5-team final-exponentiation wave, one inversion block) gives the one-kernel
+    form's codes."""
+    from handel_amd.engine import Engine
+
+    split = Engine(device=0, flavor="go")
+    try:
+        assert engine.set_message(F.LIB_MESSAGE) == 0
+        assert split.set_message(F.LIB_MESSAGE) == 0
+        split.set_verify_split(True)
+        _, pks, sigs = F.keys_and_sigs(7, seed=b"split-small")
+        sigs = F.tamper(sigs, every=3)
+        for n in (1, 7):
+            want = engine.verify_batch(pks[:128 * n], sigs[:64 * n])
+            assert list(split.verify_batch(pks[:128 * n], sigs[:64 * n])) == list(want)
+        assert list(want) == list(R.verify_batch(F.LIB_MESSAGE, pks, sigs, nthreads=4))
+    finally:
+        split.close()
