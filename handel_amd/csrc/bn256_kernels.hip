@@ -26,7 +26,10 @@ namespace hg {
 //                  all-zero => infinity; else must be on the curve.
 //   cf (cloudflare): each coordinate must be < p; all-zero => infinity; on
 //                  the curve; G2 additionally in the order-n subgroup.
-HG_DEV int32_t decode_g2_one(const uint8_t* m, int flavor, PointG2& P) {
+// The field and curve checks alone (the cf subgroup check, a scalar
+// multiplication by the group order, is left to the caller): decode_g2_one
+// and, for the pairing checks, k_decode_checks + k_checks_g2_subgroup.
+HG_DEV int32_t decode_g2_fields(const uint8_t* m, int flavor, PointG2& P) {
   bool ge[4];
   fp_from_be(P.x.x, m, &ge[0]);
   fp_from_be(P.x.y, m + 32, &ge[1]);
@@ -36,22 +39,26 @@ HG_DEV int32_t decode_g2_one(const uint8_t* m, int flavor, PointG2& P) {
   for (int k = 0; k < 128; k++) nz |= m[k] != 0;
   int32_t code = HG_OK;
   P.inf = nz ? 0u : 1u;
-  if (flavor == HG_FLAVOR_CF && (ge[0] || ge[1] || ge[2] || ge[3])) {
-    code = HG_ERR_CF_EXCEEDS;
-  } else if (nz) {
-    if (!g2_on_curve(P.x, P.y)) {
-      code = flavor == HG_FLAVOR_CF ? HG_ERR_CF_MALFORMED : HG_ERR_PK_UNMARSHAL;
-    } else if (flavor == HG_FLAVOR_CF) {
-      // order-n subgroup check (cloudflare twistPoint.IsOnCurve multiplies by Order)
-      const uint32_t order[8] = {HG_ORDER32};
-      G2J a, r;
-      a.x = P.x;
-      a.y = P.y;
-      f2_one(a.z);
-      g2_mul(r, a, order);
-      if (!g2_is_inf(r)) code = HG_ERR_CF_MALFORMED;
-    }
-  }
+  if (flavor == HG_FLAVOR_CF && (ge[0] || ge[1] || ge[2] || ge[3])) code = HG_ERR_CF_EXCEEDS;
+  else if (nz && !g2_on_curve(P.x, P.y)) code = flavor == HG_FLAVOR_CF ? HG_ERR_CF_MALFORMED : HG_ERR_PK_UNMARSHAL;
+  return code;
+}
+
+// n * P == inf for an affine point on the twist (cloudflare twistPoint.IsOnCurve
+// multiplies by Order)
+HG_DEV bool g2_in_subgroup(const PointG2& P) {
+  const uint32_t order[8] = {HG_ORDER32};
+  G2J a, r;
+  a.x = P.x;
+  a.y = P.y;
+  f2_one(a.z);
+  g2_mul(r, a, order);
+  return g2_is_inf(r);
+}
+
+HG_DEV int32_t decode_g2_one(const uint8_t* m, int flavor, PointG2& P) {
+  int32_t code = decode_g2_fields(m, flavor, P);
+  if (code == HG_OK && flavor == HG_FLAVOR_CF && !P.inf && !g2_in_subgroup(P)) code = HG_ERR_CF_MALFORMED;
   return code;
 }
 
@@ -113,6 +120,21 @@ __global__ __launch_bounds__(64) void k_agg_prologue(const AggRequest* reqs, int
   codes[i] = code;
 }
 
+// cf only, after k_decode_checks: a pk that passed the field and curve checks
+// but lies outside the order-n subgroup is HG_ERR_CF_MALFORMED, ahead of any
+// signature error (pk errors come first). Its own kernel so that the decode
+// kernel stays small: the scalar multiplication needs ~415 VGPRs, a whole
+// SIMD's file, which inside k_decode_checks made every decode wave (go flavor
+// included) wait for a SIMD the pairing waves of other batches had left empty.
+__global__ __launch_bounds__(64) void k_checks_g2_subgroup(const CheckIn* in, int n, int32_t* codes) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t c = codes[i];
+  if (c == HG_ERR_CF_EXCEEDS || c == HG_ERR_CF_MALFORMED) return;  // the pk's own error already
+  const PointG2 P = in[i].pk;
+  if (!P.inf && !g2_in_subgroup(P)) codes[i] = HG_ERR_CF_MALFORMED;
+}
+
 // The pairing-check inputs in one pass (hg_verify_batch*): 64 checks per
 // 128-thread block, wave 0 decodes the pks and wave 1 the sigs (the two run
 // side by side instead of one after the other), straight into CheckIn; pk
@@ -128,7 +150,7 @@ __global__ __launch_bounds__(128) void k_decode_checks(const uint8_t* pks, const
   if (i < n) {
     if (pk_wave) {
       PointG2 Q;
-      a = decode_g2_one(pks + (size_t)i * 128, flavor, Q);
+      a = decode_g2_fields(pks + (size_t)i * 128, flavor, Q);  // cf subgroup: k_checks_g2_subgroup
       out[i].pk = Q;
     } else {
       PointG1 S;
@@ -812,7 +834,9 @@ void launch_agg_prologue(const AggRequest* reqs, int n, uint32_t nreg, const uin
 }
 void launch_decode_checks(const uint8_t* pks, const uint8_t* sigs, int n, int flavor, CheckIn* out, int32_t* codes,
                           hipStream_t s) {
-  if (n > 0) k_decode_checks<<<nblk(n, 64), 128, 0, s>>>(pks, sigs, n, flavor, out, codes);
+  if (n <= 0) return;
+  k_decode_checks<<<nblk(n, 64), 128, 0, s>>>(pks, sigs, n, flavor, out, codes);
+  if (flavor == HG_FLAVOR_CF) k_checks_g2_subgroup<<<nblk(n, 64), 64, 0, s>>>(out, n, codes);
 }
 void launch_encode_g2(const PointG2* in, int n, uint8_t* out, hipStream_t s) {
   if (n > 0) k_encode_g2<<<nblk(n, 64), 64, 0, s>>>(in, n, out);

@@ -169,3 +169,35 @@ def test_prepare_aggregate_msg_one_lock_hold(engine):
     sig = O.g1_marshal(O.g1_mul(h, sum(ks[:8]) % O.ORDER))
     reqs = np.array([(0, 8, 8, 0)], dtype=REQ_DTYPE)
     assert list(engine.verify_aggregate(reqs, np.array([0xff], dtype=np.uint64), sig)) == [0]
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_cf_single_checks_reject_non_g2_keys(engine_cf, split):
+    """Config 2 under cloudflare's rules (hg_verify_batch: k_decode_checks,
+    then k_checks_g2_subgroup for the subgroup rule): a pk on the twist but
+    outside G2 is "bn256: malformed point" (code 8) ahead of any signature
+    error, in both check forms, and every verdict matches the C restatement."""
+    ks, reg = _crafted_registry(16)
+    pks = [reg[128 * i:128 * i + 128] for i in range(16)]
+    assert engine_cf.set_message(F.LIB_MESSAGE) == 0
+    h = O.hashed_message(F.LIB_MESSAGE)[0]
+    good = [O.g1_marshal(O.g1_mul(h, k)) if k is not None else bytes(64) for k in ks]
+    off_curve = (1).to_bytes(32, "big") + (1).to_bytes(32, "big")
+    # every key with its own signature, then the three non-G2 keys with a
+    # malformed signature and a valid key with one
+    pk_b = b"".join(pks) + pks[10] + pks[11] + pks[12] + pks[0]
+    sig_b = b"".join(good) + off_curve + good[0] + bytes(64) + off_curve
+    engine_cf.set_verify_split(split)
+    try:
+        got = list(engine_cf.verify_batch(pk_b, sig_b))
+    finally:
+        engine_cf.set_verify_split(False)
+    # the C restatement's batch entry reports decode errors coarsely (4: the
+    # pk, 5: the signature); the engine reports cloudflare's own error values
+    # (7-9 for the pk, 10-12 for the signature: hg_code_string), so compare
+    # through that mapping, verdicts exactly
+    coarse = {7: 4, 8: 4, 9: 4, 10: 5, 11: 5, 12: 5}
+    want = list(R.verify_batch(F.LIB_MESSAGE, pk_b, sig_b, nthreads=4, flavor=1))
+    assert [coarse.get(int(c), int(c)) for c in got] == [int(c) for c in want]
+    assert [got[i] for i in (10, 11, 12, 16, 17, 18)] == [8] * 6
+    assert got[19] == 11 and got[0] == 0  # a valid key with an off-curve signature
