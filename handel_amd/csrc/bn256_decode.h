@@ -12,10 +12,9 @@ namespace hg {
 // infinity; otherwise the point must be on y^2 = x^3 + 3.
 HG_DEV int32_t decode_g1_one(const uint8_t* m, int flavor, PointG1& P) {
   bool gx, gy;
-  fp_from_be(P.x, m, &gx);
-  fp_from_be(P.y, m + 32, &gy);
-  bool nz = false;
-  for (int k = 0; k < 64; k++) nz |= m[k] != 0;
+  bool nz = false;  // some byte nonzero (all-zero = infinity)
+  fp_from_be(P.x, m, &gx, &nz);
+  fp_from_be(P.y, m + 32, &gy, &nz);
   int32_t code = HG_OK;
   P.inf = nz ? 0u : 1u;
   // every G1 point this API decodes is a signature: cloudflare's

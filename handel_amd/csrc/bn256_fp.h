@@ -323,10 +323,18 @@ HG_DEV void fp_inv(Fp& r, const Fp& a) {
 }
 // big-endian 32 bytes -> LE words; returns true when the value is >= p
 HG_DEV bool be_to_words(uint32_t* w, const uint8_t* b) {
+  if ((reinterpret_cast<uintptr_t>(b) & 3) == 0) {
+    // the marshals' usual case (32-byte coordinates at 4-byte aligned
+    // offsets): eight dword loads instead of 32 byte loads
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(b);
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint8_t* q = b + (7 - i) * 4;
-    w[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    for (int i = 0; i < 8; i++) w[i] = __builtin_bswap32(q[7 - i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint8_t* q = b + (7 - i) * 4;
+      w[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
   }
   const uint32_t pw[8] = {HG_P32};
   uint32_t br = 0;
@@ -349,9 +357,16 @@ HG_DEV void words_to_be(uint8_t* b, const uint32_t* w) {
 }
 // decode 32 BE bytes into a Montgomery element (value taken mod p); *ge_p set
 // when the encoded integer is >= p (cloudflare rejects those)
-HG_DEV void fp_from_be(Fp& r, const uint8_t* b, bool* ge_p) {
+// nz_p (optional): OR-ed with "some byte of the coordinate is nonzero"
+HG_DEV void fp_from_be(Fp& r, const uint8_t* b, bool* ge_p, bool* nz_p = nullptr) {
   uint32_t w[8];
   *ge_p = be_to_words(w, b);
+  if (nz_p) {
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) any |= w[i];
+    *nz_p |= any != 0;
+  }
   Fp x;
   words_to_limbs(x, w);
   fp_to_mont(r, x);

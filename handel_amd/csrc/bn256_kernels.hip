@@ -31,12 +31,11 @@ namespace hg {
 // and, for the pairing checks, k_decode_checks + k_checks_g2_subgroup.
 HG_DEV int32_t decode_g2_fields(const uint8_t* m, int flavor, PointG2& P) {
   bool ge[4];
-  fp_from_be(P.x.x, m, &ge[0]);
-  fp_from_be(P.x.y, m + 32, &ge[1]);
-  fp_from_be(P.y.x, m + 64, &ge[2]);
-  fp_from_be(P.y.y, m + 96, &ge[3]);
-  bool nz = false;
-  for (int k = 0; k < 128; k++) nz |= m[k] != 0;
+  bool nz = false;  // some byte nonzero (all-zero = infinity)
+  fp_from_be(P.x.x, m, &ge[0], &nz);
+  fp_from_be(P.x.y, m + 32, &ge[1], &nz);
+  fp_from_be(P.y.x, m + 64, &ge[2], &nz);
+  fp_from_be(P.y.y, m + 96, &ge[3], &nz);
   int32_t code = HG_OK;
   P.inf = nz ? 0u : 1u;
   if (flavor == HG_FLAVOR_CF && (ge[0] || ge[1] || ge[2] || ge[3])) code = HG_ERR_CF_EXCEEDS;
